@@ -1,0 +1,194 @@
+/*
+ * maddpg_hip.h -- C ABI of libmaddpg_hip.so, the MI355X-native MADDPG hot path.
+ *
+ * The reference (adolfogonzalez3/maddpg) is pure Python over TensorFlow 1.x;
+ * its "plugin" boundary for this path is the Python surface of
+ *   maddpg/__init__.py:1-15               AgentTrainer
+ *   maddpg/trainer/maddpg.py:112-196      MADDPGAgentTrainer(action/experience/preupdate/update)
+ *   maddpg/trainer/replay_buffer.py:5-85  ReplayBuffer(add/make_index/sample_index/__len__)
+ *   experiments/train.py:78-189           the training loop (env step + updates)
+ * There is no reference FFI; the binding a maintainer adds is the ctypes stub
+ * in maddpg_amd/_lib.py (shown in INTEGRATION.md).  Each entry point below
+ * names the reference call it replaces.
+ *
+ * Conventions
+ *  - All compute state lives in ONE device arena the caller allocates (a
+ *    PyTorch uint8 CUDA tensor in practice) of mdp_arena_bytes() bytes; the
+ *    library never allocates device memory itself.
+ *  - "_dev" pointers are device pointers on the handle's device; "_host"
+ *    pointers are host memory.  Device-pointer calls are asynchronous on the
+ *    handle's stream unless stated; host-pointer calls synchronise.
+ *  - Return 0 on success, 1 for "skipped" (update gates), <0 on error; the
+ *    message is in mdp_last_error(h).  No C++ exception crosses the ABI.
+ *  - One handle per GPU process; calls on one handle are not thread-safe.
+ */
+#ifndef MADDPG_HIP_H
+#define MADDPG_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDP_MAX_AGENTS 8
+#define MDP_ACT_DIM 5          /* MPE Discrete(dim_p*2+1) action spaces */
+#define MDP_ABI_VERSION 1
+
+enum mdp_scenario {
+    MDP_SCN_NONE = 0,          /* trainer only (no device env) */
+    MDP_SCN_SIMPLE = 1,
+    MDP_SCN_SPREAD = 2,
+    MDP_SCN_ADVERSARY = 3,
+    MDP_SCN_TAG = 4
+};
+
+/* which parameter set of one agent (mdp_set_params / mdp_get_params) */
+enum mdp_which {
+    MDP_ACTOR = 0, MDP_CRITIC = 1, MDP_TGT_ACTOR = 2, MDP_TGT_CRITIC = 3,
+    MDP_M_ACTOR = 4, MDP_V_ACTOR = 5, MDP_M_CRITIC = 6, MDP_V_CRITIC = 7,
+    MDP_G_ACTOR = 8, MDP_G_CRITIC = 9
+};
+
+/* arena regions (mdp_region) */
+enum mdp_region_id {
+    MDP_R_THETA = 0, MDP_R_TARGET = 1, MDP_R_ADAM_M = 2, MDP_R_ADAM_V = 3,
+    MDP_R_GRAD = 4, MDP_R_REPLAY = 5, MDP_R_INDEX = 6, MDP_R_STATS = 7,
+    MDP_R_ENV = 8, MDP_R_EPLOG = 9, MDP_R_BETA = 10, MDP_R_SLAB = 11,
+    MDP_R_CTL = 12, MDP_R_COUNT = 13
+};
+
+typedef struct mdp_config {
+    int32_t n_agents;                 /* env.n (train.py:83) */
+    int32_t obs_dim[MDP_MAX_AGENTS];  /* obs_shape_n (maddpg.py:113) */
+    int32_t local_q[MDP_MAX_AGENTS];  /* local_q_func = ddpg (train.py:67-74) */
+    int32_t act_dim;                  /* must be MDP_ACT_DIM */
+    int32_t num_units;                /* --num-units (64 or 128) */
+    int32_t batch_size;               /* --batch-size */
+    int32_t max_episode_len;          /* --max-episode-len */
+    int64_t capacity;                 /* ReplayBuffer(1e6) (maddpg.py:147) */
+    int32_t num_envs;                 /* vector env copies on this rank (0: no env) */
+    int32_t scenario;                 /* enum mdp_scenario */
+    int32_t num_adversaries;          /* simple_tag / simple_adversary split */
+    int32_t world_size, rank;         /* data-parallel group (grads scaled by 1/world) */
+    float lr;                         /* --lr (Adam) */
+    float tau;                        /* Polyak 1e-2 (maddpg.py:21) */
+    float grad_clip;                  /* 0.5 (maddpg.py:130,142) */
+    float actor_reg;                  /* 1e-3 (maddpg.py:56) */
+    float adam_b1, adam_b2, adam_eps; /* TF1 AdamOptimizer defaults */
+    double gamma;                     /* --gamma (TD target in fp64, maddpg.py:186) */
+    uint64_t seed;                    /* device Philox key (Gumbel noise, env resets) */
+} mdp_config;
+
+typedef struct mdp_tensor_info {      /* one fully_connected{,_1,_2}/{weights,biases} */
+    int64_t offset;                   /* floats from the start of a param-space region */
+    int32_t rows, cols;
+} mdp_tensor_info;
+
+typedef struct mdp_handle mdp_handle;
+
+/* ---- lifecycle ------------------------------------------------------- */
+int32_t mdp_abi_version(void);
+/* arena size for cfg; fills *param_floats with the param-space length (may be NULL) */
+int64_t mdp_arena_bytes(const mdp_config* cfg, int64_t* param_floats);
+/* U.initialize() / MADDPGAgentTrainer.__init__ (maddpg.py:113-149): binds the
+ * arena, zeroes it, sets Adam beta powers, seeds the index RNG with seed. */
+int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes,
+               void* hip_stream, mdp_handle** out);
+int mdp_destroy(mdp_handle* h);
+const char* mdp_last_error(const mdp_handle* h);
+void* mdp_stream(mdp_handle* h);
+int mdp_synchronize(mdp_handle* h);
+/* byte offset + size of a region inside the arena */
+int mdp_region(const mdp_handle* h, int32_t region, int64_t* offset, int64_t* bytes);
+/* layout of tensor t (0..5 = W1,b1,W2,b2,W3,b3) of agent's actor (net=0) or critic (net=1) */
+int mdp_tensor(const mdp_handle* h, int32_t agent, int32_t net, int32_t t, mdp_tensor_info* out);
+/* joint replay row layout: offsets (floats) of agent's obs/act/obs_next/rew/done, row stride */
+int mdp_row_layout(const mdp_handle* h, int32_t agent, int32_t out6[6]);
+
+/* ---- parameters (golden injection, checkpoint; tf_util.py:259-273) --- */
+int mdp_set_params(mdp_handle* h, int32_t agent, int32_t which, const float* src_host, int64_t n);
+int mdp_get_params(mdp_handle* h, int32_t agent, int32_t which, float* dst_host, int64_t n);
+/* beta1^t, beta2^t of agent's actor (net=0) / critic (net=1) Adam */
+int mdp_get_beta_powers(mdp_handle* h, int32_t agent, int32_t net, float out2[2]);
+int mdp_set_beta_powers(mdp_handle* h, int32_t agent, int32_t net, const float in2[2]);
+
+/* ---- replay buffer (replay_buffer.py) -------------------------------- */
+int64_t mdp_buffer_len(mdp_handle* h);                     /* __len__ :18-19 */
+/* add `rows` whole joint rows [rows][row_stride] (device) at the ring head (:25-32) */
+int mdp_buffer_add_rows(mdp_handle* h, const float* rows_dev, int64_t rows);
+/* write agent's columns of arbitrary ring positions (per-agent add of the facade) */
+int mdp_buffer_put_agent(mdp_handle* h, int32_t agent, const int64_t* pos_dev,
+                         const float* cols_dev, int64_t rows);
+/* host-tracked ring state after put_agent (len/next are per agent in the reference) */
+int mdp_buffer_set_len(mdp_handle* h, int64_t len, int64_t next_idx);
+/* random.seed(seed) on the device MT19937 (CPython init_by_array) */
+int mdp_seed_py_random(mdp_handle* h, uint64_t seed);
+/* random.setstate/getstate: 624 words + position (random.getstate()[1]) */
+int mdp_set_rng_state(mdp_handle* h, const uint32_t* state625_host);
+int mdp_get_rng_state(mdp_handle* h, uint32_t* state625_host);
+/* make_index (:46-47): count x randint(0, len-1), bit-exact CPython stream */
+int mdp_make_index(mdp_handle* h, int32_t count, int32_t* idx_dev);
+/* sample_index (:55-56) fused gather: out[b] = joint row idx[b] */
+int mdp_sample_rows(mdp_handle* h, const int32_t* idx_dev, int32_t count, float* out_dev);
+
+/* ---- policies (maddpg.py:151-152, p_debug / q_debug) ------------------ */
+/* act[rows][5] = gumbel_softmax(actor_or_target(obs)); u_dev: injected uniforms or NULL */
+int mdp_act(mdp_handle* h, int32_t agent, int32_t target, const float* obs_dev,
+            float* act_dev, int32_t rows, const float* u_dev);
+/* logits[rows][5] = actor_or_target(obs) (p_debug['p_values'], maddpg.py:63) */
+int mdp_actor_logits(mdp_handle* h, int32_t agent, int32_t target, const float* obs_dev,
+                     float* logits_dev, int32_t rows);
+/* q[rows] = critic_or_target(x[rows][cin]) with x already concatenated */
+int mdp_q_values(mdp_handle* h, int32_t agent, int32_t target, const float* x_dev,
+                 float* q_dev, int32_t rows);
+
+/* ---- training (maddpg.py:161-196) ------------------------------------ */
+/* One agent's update past the gates, strict reference order.
+ * idx_dev: B indices or NULL (draw from the device MT stream);
+ * u_tgt_dev: [n_agents][B][5] uniforms for the target actors or NULL;
+ * u_act_dev: [B][5] uniforms for the actor-loss sample or NULL. */
+int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev,
+               const float* u_tgt_dev, const float* u_act_dev);
+/* gates of maddpg.py:162-165; returns 1 (skip) or 0 (train) */
+int mdp_update_gate(mdp_handle* h, int64_t t);
+/* update round: all agents in order (train.py:158-161), indices from the MT stream */
+int mdp_update_round(mdp_handle* h);
+/* phase entry points for data parallelism (grad -> all-reduce -> apply) */
+int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev);
+int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev);
+/* reduce the per-workgroup partials of net (0 actor, 1 critic) into MDP_R_GRAD */
+int mdp_reduce_grad(mdp_handle* h, int32_t agent, int32_t net);
+/* clip + Adam (+ Polyak of both nets when net==0) reading MDP_R_GRAD scaled by `scale` */
+int mdp_apply_grad(mdp_handle* h, int32_t agent, int32_t net, float scale);
+/* the 6 values update() returns (maddpg.py:196), fp64, synchronises */
+int mdp_get_stats(mdp_handle* h, int32_t agent, double out6[6]);
+
+/* ---- device environments (MPE World.step, train.py:104-128) ---------- */
+int mdp_env_reset(mdp_handle* h);
+/* one vector step: actions from the actors (or act_in_dev [E][n][5]), physics,
+ * replay append, episode bookkeeping and resets at max_episode_len.
+ * u_dev: injected Gumbel uniforms [E][n][5] or NULL. */
+int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev);
+/* env state: pos/vel [E][n_entities][2] fp32, goal [E] int32, ep_step [E] int32 */
+int mdp_env_get_state(mdp_handle* h, float* pos_host, float* vel_host, int32_t* goal_host, int32_t* ep_step_host);
+int mdp_env_set_state(mdp_handle* h, const float* pos_host, const float* vel_host, const int32_t* goal_host, const int32_t* ep_step_host);
+int mdp_env_obs(mdp_handle* h, float* obs_dev);   /* current obs [E][sum obs] */
+/* finished-episode log: total entries written so far, copy last `n` [n][1+n_agents] */
+int64_t mdp_episode_count(mdp_handle* h);
+int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out_host);
+
+/* ---- profiling: HIP events bracketing every launch of one kernel kind -- */
+enum mdp_kernel_kind {
+    MDP_K_INDEX = 0, MDP_K_GATHER = 1, MDP_K_CRITIC_GRAD = 2, MDP_K_ACTOR_GRAD = 3,
+    MDP_K_APPLY = 4, MDP_K_ROLLOUT = 5, MDP_K_REDUCE = 6, MDP_K_COUNT = 7
+};
+int mdp_prof_enable(mdp_handle* h, int32_t kind, int32_t on);
+/* sum of event-measured durations (ms) and launch count since enable; synchronises */
+int mdp_prof_read(mdp_handle* h, int32_t kind, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MADDPG_HIP_H */

@@ -1,0 +1,984 @@
+// mdp_api.cpp -- C ABI of libmaddpg_hip.so (declared in include/maddpg_hip.h).
+//
+// Owns the handle: arena carving, parameter/replay layout, the device MT19937
+// control block, launch sequencing for the reference's per-agent update
+// order (maddpg.py:161-196, train.py:158-161), the device env loop and the
+// HIP-event kernel timers used by bench.py.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mdp_kernels.h"
+
+namespace {
+
+inline int64_t r4(int64_t n) { return (n + 3) & ~int64_t(3); }
+inline int64_t a256(int64_t n) { return (n + 255) & ~int64_t(255); }
+
+NDesc make_net(int64_t& off, int in, int H, int out) {
+  NDesc d;
+  d.off = (int)off;
+  d.in = in;
+  d.out = out;
+  const int shp[6][2] = {{in, H}, {1, H}, {H, H}, {1, H}, {H, out}, {1, out}};
+  for (int t = 0; t < 6; ++t) {
+    d.t[t].off = (int)off;
+    d.t[t].rows = shp[t][0];
+    d.t[t].cols = shp[t][1];
+    off += r4((int64_t)shp[t][0] * shp[t][1]);
+  }
+  d.size = (int)(off - d.off);
+  return d;
+}
+
+// scenario entity tables (multiagent/scenarios/*.py make_world)
+bool make_env(const mdp_config& c, EnvDesc& e, std::vector<int>& obs_dims, std::string& err) {
+  std::memset(&e, 0, sizeof(e));
+  e.scenario = c.scenario;
+  e.max_ep_len = c.max_episode_len;
+  const int n = c.n_agents;
+  e.n_agents = n;
+  for (int i = 0; i < MDP_MAX_ENT; ++i) e.max_speed[i] = -1.f;
+  for (int i = 0; i < MDP_MAX_AGENTS; ++i) e.accel[i] = 5.0f;
+  obs_dims.assign(n, 0);
+  switch (c.scenario) {
+    case MDP_SCN_SIMPLE:
+      if (n != 1) { err = "simple has exactly 1 agent"; return false; }
+      e.n_landmarks = 1;
+      e.size[0] = e.size[1] = 0.05f;
+      e.movable[0] = 1;
+      obs_dims[0] = 4;
+      break;
+    case MDP_SCN_SPREAD:
+      e.n_landmarks = n;
+      for (int i = 0; i < n; ++i) {
+        e.size[i] = 0.15f;
+        e.collide[i] = 1;
+        e.movable[i] = 1;
+        e.size[n + i] = 0.05f;
+        obs_dims[i] = 4 + 2 * n + 4 * (n - 1);
+      }
+      break;
+    case MDP_SCN_ADVERSARY: {
+      const int na = c.num_adversaries;
+      if (na < 1 || na >= n) { err = "simple_adversary needs 1 <= adversaries < agents"; return false; }
+      e.n_landmarks = n - 1;
+      e.n_adv = na;
+      for (int i = 0; i < n; ++i) {
+        e.size[i] = 0.15f;
+        e.movable[i] = 1;
+        e.adversary[i] = i < na;
+        obs_dims[i] = (i < na ? 0 : 2) + 2 * (n - 1) + 2 * (n - 1);
+      }
+      for (int l = 0; l < n - 1; ++l) e.size[n + l] = 0.08f;
+      break;
+    }
+    case MDP_SCN_TAG: {
+      const int na = c.num_adversaries, ng = n - na, L = 2;
+      if (na < 1 || ng < 1) { err = "simple_tag needs >=1 adversary and >=1 good agent"; return false; }
+      e.n_landmarks = L;
+      e.n_adv = na;
+      for (int i = 0; i < n; ++i) {
+        const bool adv = i < na;
+        e.adversary[i] = adv;
+        e.size[i] = adv ? 0.075f : 0.05f;
+        e.accel[i] = adv ? 3.0f : 4.0f;
+        e.max_speed[i] = adv ? 1.0f : 1.3f;
+        e.collide[i] = 1;
+        e.movable[i] = 1;
+        obs_dims[i] = 4 + 2 * L + 2 * (n - 1) + 2 * (adv ? ng : ng - 1);
+      }
+      for (int l = 0; l < L; ++l) {
+        e.size[n + l] = 0.2f;
+        e.collide[n + l] = 1;
+      }
+      break;
+    }
+    default:
+      err = "unknown scenario";
+      return false;
+  }
+  if (n + e.n_landmarks > MDP_MAX_ENT) { err = "too many entities"; return false; }
+  return true;
+}
+
+struct Layout {
+  Topo topo;
+  EnvDesc env;
+  int64_t PT = 0;
+  int nwg = 0, slab_c = 0, slab_a = 0, eplog_rows = 0, n_ent = 0;
+  int64_t off[MDP_R_COUNT];
+  int64_t bytes[MDP_R_COUNT];
+  int64_t total = 0;
+};
+
+bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
+  if (!c) { err = "null config"; return false; }
+  if (c->n_agents < 1 || c->n_agents > MDP_MAX_AGENTS) { err = "n_agents out of range"; return false; }
+  if (c->act_dim != MDP_ACT_DIM) { err = "act_dim must be 5 (MPE Discrete(5))"; return false; }
+  if (c->num_units != 64 && c->num_units != 128) { err = "num_units must be 64 or 128"; return false; }
+  if (c->batch_size < 1) { err = "batch_size must be >= 1"; return false; }
+  if (c->capacity < 1 || c->capacity > (int64_t(1) << 31) - 1) { err = "capacity out of range"; return false; }
+  if (c->num_envs < 0) { err = "num_envs < 0"; return false; }
+  const int n = c->n_agents, H = c->num_units;
+  Topo& T = L.topo;
+  std::memset(&T, 0, sizeof(T));
+  T.n = n;
+  T.H = H;
+  int sum_obs = 0, obs_max = 0;
+  for (int i = 0; i < n; ++i) {
+    if (c->obs_dim[i] < 1 || c->obs_dim[i] > 256) { err = "obs_dim out of range"; return false; }
+    sum_obs += c->obs_dim[i];
+    obs_max = std::max(obs_max, (int)c->obs_dim[i]);
+  }
+  T.sum_obs = sum_obs;
+  T.obs_max = obs_max;
+  T.row_stride = (int)r4(2 * sum_obs + (MDP_ACT_DIM + 2) * n);
+  int64_t off = 0;
+  int acc = 0, cin_max = 0;
+  for (int i = 0; i < n; ++i) {
+    ADesc& a = T.ag[i];
+    a.obs_dim = c->obs_dim[i];
+    a.local_q = c->local_q[i] ? 1 : 0;
+    a.obs_off = acc;
+    a.act_off = sum_obs + MDP_ACT_DIM * i;
+    a.nobs_off = sum_obs + MDP_ACT_DIM * n + acc;
+    a.rew_off = 2 * sum_obs + MDP_ACT_DIM * n + i;
+    a.done_off = 2 * sum_obs + MDP_ACT_DIM * n + n + i;
+    acc += a.obs_dim;
+    a.cin = a.local_q ? a.obs_dim + MDP_ACT_DIM : sum_obs + MDP_ACT_DIM * n;
+    a.a_in_off = a.local_q ? a.obs_dim : sum_obs + MDP_ACT_DIM * i;
+    cin_max = std::max(cin_max, a.cin);
+    a.actor = make_net(off, a.obs_dim, H, MDP_ACT_DIM);
+    a.critic = make_net(off, a.cin, H, 1);
+  }
+  T.cin_max = cin_max;
+  L.PT = off;
+  L.nwg = (c->batch_size + 15) / 16;
+  for (int i = 0; i < n; ++i) {
+    L.slab_c = std::max(L.slab_c, T.ag[i].critic.size);
+    L.slab_a = std::max(L.slab_a, T.ag[i].actor.size);
+  }
+  const int E = c->num_envs;
+  std::vector<int> dims;
+  if (c->scenario != MDP_SCN_NONE) {
+    if (!make_env(*c, L.env, dims, err)) return false;
+    for (int i = 0; i < n; ++i)
+      if (dims[i] != c->obs_dim[i]) {
+        char b[160];
+        std::snprintf(b, sizeof(b), "obs_dim[%d]=%d does not match scenario (%d)", i, c->obs_dim[i], dims[i]);
+        err = b;
+        return false;
+      }
+    if ((int64_t)E > c->capacity) { err = "num_envs exceeds replay capacity"; return false; }
+  } else {
+    std::memset(&L.env, 0, sizeof(L.env));
+  }
+  L.n_ent = n + L.env.n_landmarks;
+  L.eplog_rows = std::max(4096, 4 * E);
+  int64_t sz[MDP_R_COUNT];
+  sz[MDP_R_THETA] = sz[MDP_R_TARGET] = sz[MDP_R_ADAM_M] = sz[MDP_R_ADAM_V] = sz[MDP_R_GRAD] = 4 * L.PT;
+  sz[MDP_R_REPLAY] = 4 * c->capacity * T.row_stride;
+  sz[MDP_R_INDEX] = 4 * (int64_t)n * c->batch_size;
+  sz[MDP_R_STATS] = 8 * 8 * (int64_t)n;
+  sz[MDP_R_ENV] = (int64_t)E * (4 * 4 * L.n_ent + 4 + 4 + 4 * n) + 64;
+  sz[MDP_R_EPLOG] = 4 * (int64_t)L.eplog_rows * (1 + n);
+  sz[MDP_R_BETA] = 4 * 4 * (int64_t)n;
+  sz[MDP_R_SLAB] = 4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg + 8 * (int64_t)c->batch_size + 256;
+  sz[MDP_R_CTL] = sizeof(Ctl);
+  int64_t o = 0;
+  for (int r = 0; r < MDP_R_COUNT; ++r) {
+    L.off[r] = o;
+    L.bytes[r] = sz[r];
+    o += a256(sz[r]);
+  }
+  L.total = o;
+  return true;
+}
+
+// CPython _randommodule.c: init_genrand + init_by_array, key = 32-bit words of |seed|
+void py_seed_state(uint64_t seed, uint32_t* mt, int32_t* pos) {
+  std::vector<uint32_t> key;
+  uint64_t s = seed;
+  while (s) {
+    key.push_back((uint32_t)(s & 0xffffffffu));
+    s >>= 32;
+  }
+  if (key.empty()) key.push_back(0);
+  mt[0] = 19650218u;
+  for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+  int i = 1, j = 0;
+  const int kl = (int)key.size();
+  for (int k = std::max(624, kl); k; --k) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+    ++i;
+    ++j;
+    if (i >= 624) {
+      mt[0] = mt[623];
+      i = 1;
+    }
+    if (j >= kl) j = 0;
+  }
+  for (int k = 623; k; --k) {
+    mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+    ++i;
+    if (i >= 624) {
+      mt[0] = mt[623];
+      i = 1;
+    }
+  }
+  mt[0] = 0x80000000u;
+  *pos = 624;
+}
+
+}  // namespace
+
+struct mdp_handle {
+  mdp_config cfg;
+  Layout L;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  char* arena = nullptr;
+  float *theta, *target, *m, *v, *grad, *replay, *beta, *slab_c, *slab_a, *eplog;
+  float *pos, *vel, *ep_rew;
+  int32_t *index, *goal, *ep_step;
+  double *stats, *stat_c, *stat_a, *y;
+  Ctl* ctl;
+  int64_t len = 0, next = 0;  // host mirror of the ring
+  uint32_t act_ctr = 0, reset_ctr = 0;
+  std::string err;
+  bool prof_on[MDP_K_COUNT] = {};
+  std::vector<hipEvent_t> ev[MDP_K_COUNT];
+  size_t ev_used[MDP_K_COUNT] = {};
+  double prof_ms[MDP_K_COUNT] = {};
+  int64_t prof_n[MDP_K_COUNT] = {};
+};
+
+namespace {
+
+int fail(mdp_handle* h, const char* what, hipError_t e = hipSuccess) {
+  if (h) {
+    h->err = what;
+    if (e != hipSuccess) {
+      h->err += ": ";
+      h->err += hipGetErrorString(e);
+    }
+  }
+  return -1;
+}
+
+#define HIPCHK(h, call)                        \
+  do {                                         \
+    hipError_t e__ = (call);                   \
+    if (e__ != hipSuccess) return fail(h, #call, e__); \
+  } while (0)
+
+// bracket one launch with timing events when profiling `kind`
+struct ProfScope {
+  mdp_handle* h;
+  int kind;
+  hipEvent_t stop = nullptr;
+  ProfScope(mdp_handle* hh, int k) : h(hh), kind(k) {
+    if (!h->prof_on[kind]) return;
+    auto& pool = h->ev[kind];
+    size_t u = h->ev_used[kind];
+    if (u + 2 > pool.size()) {
+      for (int q = 0; q < 64; ++q) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        pool.push_back(e);
+      }
+    }
+    (void)hipEventRecord(pool[u], h->stream);
+    stop = pool[u + 1];
+    h->ev_used[kind] = u + 2;
+  }
+  ~ProfScope() {
+    if (stop) (void)hipEventRecord(stop, h->stream);
+  }
+};
+
+void flush_prof(mdp_handle* h, int kind) {
+  auto& pool = h->ev[kind];
+  const size_t u = h->ev_used[kind];
+  if (!u) return;
+  (void)hipEventSynchronize(pool[u - 1]);
+  for (size_t q = 0; q + 1 < u; q += 2) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, pool[q], pool[q + 1]) == hipSuccess) {
+      h->prof_ms[kind] += ms;
+      h->prof_n[kind] += 1;
+    }
+  }
+  h->ev_used[kind] = 0;
+}
+
+bool bad_agent(mdp_handle* h, int agent) {
+  if (agent < 0 || agent >= h->cfg.n_agents) {
+    fail(h, "agent index out of range");
+    return true;
+  }
+  return false;
+}
+
+int region_for(int which, int* region, int* net) {
+  switch (which) {
+    case MDP_ACTOR: *region = MDP_R_THETA; *net = 0; return 0;
+    case MDP_CRITIC: *region = MDP_R_THETA; *net = 1; return 0;
+    case MDP_TGT_ACTOR: *region = MDP_R_TARGET; *net = 0; return 0;
+    case MDP_TGT_CRITIC: *region = MDP_R_TARGET; *net = 1; return 0;
+    case MDP_M_ACTOR: *region = MDP_R_ADAM_M; *net = 0; return 0;
+    case MDP_V_ACTOR: *region = MDP_R_ADAM_V; *net = 0; return 0;
+    case MDP_M_CRITIC: *region = MDP_R_ADAM_M; *net = 1; return 0;
+    case MDP_V_CRITIC: *region = MDP_R_ADAM_V; *net = 1; return 0;
+    case MDP_G_ACTOR: *region = MDP_R_GRAD; *net = 0; return 0;
+    case MDP_G_CRITIC: *region = MDP_R_GRAD; *net = 1; return 0;
+    default: return -1;
+  }
+}
+
+const NDesc& net_of(mdp_handle* h, int agent, int net) {
+  return net ? h->L.topo.ag[agent].critic : h->L.topo.ag[agent].actor;
+}
+
+int64_t net_floats(const NDesc& d) {
+  int64_t s = 0;
+  for (int t = 0; t < 6; ++t) s += (int64_t)d.t[t].rows * d.t[t].cols;
+  return s;
+}
+
+int launch_make_index(mdp_handle* h, int count, int32_t* out) {
+  if (h->len <= 0) return fail(h, "make_index on an empty replay buffer (randint(0, -1))");
+  ProfScope p(h, MDP_K_INDEX);
+  HIPCHK(h, mdp_launch_make_index(h->ctl, count, out, h->stream));
+  return 0;
+}
+
+int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt) {
+  CriticArgs a;
+  a.topo = h->L.topo;
+  a.agent = agent;
+  a.B = h->cfg.batch_size;
+  a.theta = h->theta;
+  a.target = h->target;
+  a.replay = h->replay;
+  a.idx = idx;
+  a.u_tgt = u_tgt;
+  a.seed = h->cfg.seed;
+  a.ctl = h->ctl;
+  a.gamma = h->cfg.gamma;
+  a.inv_b = 1.0f / (float)a.B;
+  a.slab = h->slab_c;
+  a.slab_stride = h->L.slab_c;
+  a.slab_stat = h->stat_c;
+  a.y_out = h->y;
+  ProfScope p(h, MDP_K_CRITIC_GRAD);
+  HIPCHK(h, mdp_launch_critic_grad(a, h->cfg.num_units, lds_critic_bytes(h->L.topo), h->stream));
+  return 0;
+}
+
+int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act) {
+  ActorArgs a;
+  a.topo = h->L.topo;
+  a.agent = agent;
+  a.B = h->cfg.batch_size;
+  a.theta = h->theta;
+  a.replay = h->replay;
+  a.idx = idx;
+  a.u_act = u_act;
+  a.seed = h->cfg.seed;
+  a.ctl = h->ctl;
+  a.neg_inv_b = -1.0f / (float)a.B;
+  a.reg_scale = (float)(2.0 * (double)h->cfg.actor_reg / ((double)a.B * MDP_ACT_DIM));
+  a.slab = h->slab_a;
+  a.slab_stride = h->L.slab_a;
+  a.slab_stat = h->stat_a;
+  ProfScope p(h, MDP_K_ACTOR_GRAD);
+  HIPCHK(h, mdp_launch_actor_grad(a, h->cfg.num_units, lds_actor_bytes(h->L.topo), h->stream));
+  return 0;
+}
+
+// net 1: critic Adam (+ critic stats); net 0: actor Adam + Polyak of both nets (+ actor stats)
+int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
+  const ADesc& ag = h->L.topo.ag[agent];
+  ApplyArgs a;
+  a.net = net ? ag.critic : ag.actor;
+  a.other = net ? ag.actor : ag.critic;
+  a.theta = h->theta;
+  a.target = h->target;
+  a.m = h->m;
+  a.v = h->v;
+  a.grad = h->grad;
+  a.slab = from_slab ? (net ? h->slab_c : h->slab_a) : nullptr;
+  a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
+  a.nwg = h->L.nwg;
+  a.scale = scale;
+  a.clip = h->cfg.grad_clip;
+  a.lr = h->cfg.lr;
+  a.b1 = h->cfg.adam_b1;
+  a.b2 = h->cfg.adam_b2;
+  a.eps = h->cfg.adam_eps;
+  a.beta = h->beta + agent * 4 + net * 2;
+  a.polyak = net ? 0 : 1;
+  const double tau = (double)h->cfg.tau;
+  a.pa = (float)(1.0 - tau);
+  a.pb = (float)(1.0 - (1.0 - tau));
+  a.stats_mode = net ? 1 : 2;
+  a.slab_stat = net ? h->stat_c : h->stat_a;
+  a.y = h->y;
+  a.B = h->cfg.batch_size;
+  a.reg = h->cfg.actor_reg;
+  a.stats_out = h->stats + agent * 8;
+  a.ticket = &h->ctl->ticket[net];
+  a.ctl = h->ctl;
+  a.bump_ctr = net ? 0 : 1;
+  ProfScope p(h, MDP_K_APPLY);
+  HIPCHK(h, mdp_launch_apply(a, h->stream));
+  return 0;
+}
+
+int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act) {
+  int rc;
+  if ((rc = do_critic_grad(h, agent, idx, u_tgt))) return rc;
+  if ((rc = do_apply(h, agent, 1, true, 1.0f))) return rc;
+  if ((rc = do_actor_grad(h, agent, idx, u_act))) return rc;
+  if ((rc = do_apply(h, agent, 0, true, 1.0f))) return rc;
+  return 0;
+}
+
+int set_ring(mdp_handle* h, int64_t len, int64_t next) {
+  h->len = len;
+  h->next = next;
+  HIPCHK(h, mdp_launch_set_ring(h->ctl, len, next, h->stream));
+  return 0;
+}
+
+}  // namespace
+
+// ======================================================================= ABI
+extern "C" {
+
+int32_t mdp_abi_version(void) { return MDP_ABI_VERSION; }
+
+int64_t mdp_arena_bytes(const mdp_config* cfg, int64_t* param_floats) {
+  Layout L;
+  std::string err;
+  if (!build_layout(cfg, L, err)) return -1;
+  if (param_floats) *param_floats = L.PT;
+  return L.total;
+}
+
+int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void* hip_stream, mdp_handle** out) {
+  if (!out) return -1;
+  *out = nullptr;
+  mdp_handle* h = new mdp_handle();
+  std::string err;
+  if (!build_layout(cfg, h->L, err)) {
+    h->err = err;
+    *out = h;
+    return -1;
+  }
+  h->cfg = *cfg;
+  if (!arena_dev || arena_bytes < h->L.total) {
+    h->err = "arena missing or too small";
+    *out = h;
+    return -1;
+  }
+  *out = h;
+  HIPCHK(h, hipGetDevice(&h->device));
+  if (hip_stream) {
+    h->stream = (hipStream_t)hip_stream;
+  } else {
+    HIPCHK(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->own_stream = true;
+  }
+  h->arena = (char*)arena_dev;
+  auto R = [&](int r) { return (void*)(h->arena + h->L.off[r]); };
+  h->theta = (float*)R(MDP_R_THETA);
+  h->target = (float*)R(MDP_R_TARGET);
+  h->m = (float*)R(MDP_R_ADAM_M);
+  h->v = (float*)R(MDP_R_ADAM_V);
+  h->grad = (float*)R(MDP_R_GRAD);
+  h->replay = (float*)R(MDP_R_REPLAY);
+  h->index = (int32_t*)R(MDP_R_INDEX);
+  h->stats = (double*)R(MDP_R_STATS);
+  h->eplog = (float*)R(MDP_R_EPLOG);
+  h->beta = (float*)R(MDP_R_BETA);
+  h->ctl = (Ctl*)R(MDP_R_CTL);
+  {
+    const int E = cfg->num_envs, ne = h->L.n_ent, n = cfg->n_agents;
+    char* p = (char*)R(MDP_R_ENV);
+    h->pos = (float*)p;
+    p += 4 * (int64_t)E * ne * 2;
+    h->vel = (float*)p;
+    p += 4 * (int64_t)E * ne * 2;
+    h->goal = (int32_t*)p;
+    p += 4 * (int64_t)E;
+    h->ep_step = (int32_t*)p;
+    p += 4 * (int64_t)E;
+    h->ep_rew = (float*)p;
+    (void)n;
+  }
+  {
+    char* p = (char*)R(MDP_R_SLAB);
+    const int64_t nwg = h->L.nwg;
+    h->slab_c = (float*)p;
+    p += 4 * nwg * h->L.slab_c;
+    h->slab_a = (float*)p;
+    p += 4 * nwg * h->L.slab_a;
+    p = (char*)(((uintptr_t)p + 7) & ~uintptr_t(7));
+    h->stat_c = (double*)p;
+    p += 8 * 8 * nwg;
+    h->stat_a = (double*)p;
+    p += 8 * 8 * nwg;
+    h->y = (double*)p;
+  }
+  HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
+  std::vector<float> beta(4 * cfg->n_agents);
+  for (int i = 0; i < cfg->n_agents * 2; ++i) {
+    beta[2 * i] = cfg->adam_b1;
+    beta[2 * i + 1] = cfg->adam_b2;
+  }
+  HIPCHK(h, hipMemcpyAsync(h->beta, beta.data(), 4 * beta.size(), hipMemcpyHostToDevice, h->stream));
+  Ctl c;
+  std::memset(&c, 0, sizeof(c));
+  py_seed_state(0, c.mt, &c.mt_pos);
+  HIPCHK(h, hipMemcpyAsync(h->ctl, &c, sizeof(c), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->err.clear();
+  return 0;
+}
+
+int mdp_destroy(mdp_handle* h) {
+  if (!h) return 0;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (int k = 0; k < MDP_K_COUNT; ++k)
+    for (auto e : h->ev[k]) (void)hipEventDestroy(e);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+const char* mdp_last_error(const mdp_handle* h) { return h ? h->err.c_str() : "null handle"; }
+void* mdp_stream(mdp_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int mdp_synchronize(mdp_handle* h) {
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_region(const mdp_handle* h, int32_t region, int64_t* offset, int64_t* bytes) {
+  if (!h || region < 0 || region >= MDP_R_COUNT) return -1;
+  if (offset) *offset = h->L.off[region];
+  if (bytes) *bytes = h->L.bytes[region];
+  return 0;
+}
+
+int mdp_tensor(const mdp_handle* h, int32_t agent, int32_t net, int32_t t, mdp_tensor_info* out) {
+  if (!h || agent < 0 || agent >= h->cfg.n_agents || t < 0 || t > 5 || !out) return -1;
+  const NDesc& d = net ? h->L.topo.ag[agent].critic : h->L.topo.ag[agent].actor;
+  out->offset = d.t[t].off;
+  out->rows = d.t[t].rows;
+  out->cols = d.t[t].cols;
+  return 0;
+}
+
+int mdp_row_layout(const mdp_handle* h, int32_t agent, int32_t out6[6]) {
+  if (!h || agent < 0 || agent >= h->cfg.n_agents) return -1;
+  const ADesc& a = h->L.topo.ag[agent];
+  out6[0] = a.obs_off;
+  out6[1] = a.act_off;
+  out6[2] = a.nobs_off;
+  out6[3] = a.rew_off;
+  out6[4] = a.done_off;
+  out6[5] = h->L.topo.row_stride;
+  return 0;
+}
+
+int mdp_set_params(mdp_handle* h, int32_t agent, int32_t which, const float* src, int64_t n) {
+  if (bad_agent(h, agent)) return -1;
+  int region, net;
+  if (region_for(which, &region, &net)) return fail(h, "bad param set id");
+  const NDesc& d = net_of(h, agent, net);
+  if (n != net_floats(d)) return fail(h, "param count mismatch");
+  std::vector<float> buf(d.size, 0.f);
+  int64_t s = 0;
+  for (int t = 0; t < 6; ++t) {
+    const int64_t k = (int64_t)d.t[t].rows * d.t[t].cols;
+    std::memcpy(buf.data() + (d.t[t].off - d.off), src + s, 4 * k);
+    s += k;
+  }
+  float* dst = (float*)(h->arena + h->L.off[region]) + d.off;
+  HIPCHK(h, hipMemcpyAsync(dst, buf.data(), 4 * buf.size(), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_get_params(mdp_handle* h, int32_t agent, int32_t which, float* dst, int64_t n) {
+  if (bad_agent(h, agent)) return -1;
+  int region, net;
+  if (region_for(which, &region, &net)) return fail(h, "bad param set id");
+  const NDesc& d = net_of(h, agent, net);
+  if (n != net_floats(d)) return fail(h, "param count mismatch");
+  std::vector<float> buf(d.size);
+  const float* src = (const float*)(h->arena + h->L.off[region]) + d.off;
+  HIPCHK(h, hipMemcpyAsync(buf.data(), src, 4 * buf.size(), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  int64_t s = 0;
+  for (int t = 0; t < 6; ++t) {
+    const int64_t k = (int64_t)d.t[t].rows * d.t[t].cols;
+    std::memcpy(dst + s, buf.data() + (d.t[t].off - d.off), 4 * k);
+    s += k;
+  }
+  return 0;
+}
+
+int mdp_get_beta_powers(mdp_handle* h, int32_t agent, int32_t net, float out2[2]) {
+  if (bad_agent(h, agent)) return -1;
+  HIPCHK(h, hipMemcpyAsync(out2, h->beta + agent * 4 + (net ? 2 : 0), 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_set_beta_powers(mdp_handle* h, int32_t agent, int32_t net, const float in2[2]) {
+  if (bad_agent(h, agent)) return -1;
+  HIPCHK(h, hipMemcpyAsync(h->beta + agent * 4 + (net ? 2 : 0), in2, 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// ----------------------------------------------------------------- replay
+int64_t mdp_buffer_len(mdp_handle* h) { return h ? h->len : -1; }
+
+int mdp_buffer_add_rows(mdp_handle* h, const float* rows_dev, int64_t rows) {
+  if (rows < 0) return fail(h, "negative row count");
+  if (rows == 0) return 0;
+  const int64_t cap = h->cfg.capacity;
+  // more rows than the ring holds: only the last `cap` survive (earlier ones
+  // would be overwritten), which also keeps every destination row unique
+  const int64_t skip = rows > cap ? rows - cap : 0;
+  const int64_t start = (h->next + skip) % cap;
+  HIPCHK(h, mdp_launch_put_rows(h->replay, h->L.topo.row_stride, cap, start,
+                                rows_dev + skip * h->L.topo.row_stride, rows - skip, h->stream));
+  return set_ring(h, std::min(cap, h->len + rows), (h->next + rows) % cap);
+}
+
+int mdp_buffer_put_agent(mdp_handle* h, int32_t agent, const int64_t* pos_dev, const float* cols_dev, int64_t rows) {
+  if (bad_agent(h, agent)) return -1;
+  if (rows <= 0) return 0;
+  HIPCHK(h, mdp_launch_put_agent(h->replay, h->L.topo.row_stride, h->L.topo.ag[agent], pos_dev, cols_dev, rows,
+                                 h->stream));
+  return 0;
+}
+
+int mdp_buffer_set_len(mdp_handle* h, int64_t len, int64_t next_idx) {
+  if (len < 0 || len > h->cfg.capacity || next_idx < 0 || next_idx >= h->cfg.capacity)
+    return fail(h, "ring state out of range");
+  return set_ring(h, len, next_idx);
+}
+
+int mdp_seed_py_random(mdp_handle* h, uint64_t seed) {
+  Ctl c;
+  py_seed_state(seed, c.mt, &c.mt_pos);
+  HIPCHK(h, hipMemcpyAsync(h->ctl->mt, c.mt, sizeof(c.mt) + sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_set_rng_state(mdp_handle* h, const uint32_t* st) {
+  if (st[624] > 624) return fail(h, "MT position out of range");
+  uint32_t buf[625];
+  std::memcpy(buf, st, sizeof(buf));
+  HIPCHK(h, hipMemcpyAsync(h->ctl->mt, buf, sizeof(buf), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_get_rng_state(mdp_handle* h, uint32_t* st) {
+  HIPCHK(h, hipMemcpyAsync(st, h->ctl->mt, 625 * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_make_index(mdp_handle* h, int32_t count, int32_t* idx_dev) {
+  if (count < 0) return fail(h, "negative count");
+  if (count == 0) return 0;
+  return launch_make_index(h, count, idx_dev);
+}
+
+int mdp_sample_rows(mdp_handle* h, const int32_t* idx_dev, int32_t count, float* out_dev) {
+  if (count <= 0) return 0;
+  ProfScope p(h, MDP_K_GATHER);
+  HIPCHK(h, mdp_launch_gather(h->replay, h->L.topo.row_stride, idx_dev, count, out_dev, h->stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------- policies
+int mdp_act(mdp_handle* h, int32_t agent, int32_t target, const float* obs_dev, float* act_dev, int32_t rows,
+            const float* u_dev) {
+  if (bad_agent(h, agent)) return -1;
+  if (rows <= 0) return 0;
+  const ADesc& ag = h->L.topo.ag[agent];
+  EvalArgs a;
+  a.P = target ? h->target : h->theta;
+  a.net = ag.actor;
+  a.in = ag.obs_dim;
+  a.rows = rows;
+  a.x = obs_dev;
+  a.out = act_dev;
+  a.gumbel = 1;
+  a.u = u_dev;
+  a.seed = h->cfg.seed;
+  a.stream = 0x40000u | (uint32_t)(agent << 1) | (uint32_t)(target ? 1 : 0);
+  a.ctr = h->act_ctr++;
+  HIPCHK(h, mdp_launch_eval(a, h->cfg.num_units, lds_eval_bytes(a.in, h->cfg.num_units), h->stream));
+  return 0;
+}
+
+int mdp_actor_logits(mdp_handle* h, int32_t agent, int32_t target, const float* obs_dev, float* logits_dev,
+                     int32_t rows) {
+  if (bad_agent(h, agent)) return -1;
+  if (rows <= 0) return 0;
+  const ADesc& ag = h->L.topo.ag[agent];
+  EvalArgs a;
+  a.P = target ? h->target : h->theta;
+  a.net = ag.actor;
+  a.in = ag.obs_dim;
+  a.rows = rows;
+  a.x = obs_dev;
+  a.out = logits_dev;
+  a.gumbel = 0;
+  a.u = nullptr;
+  a.seed = h->cfg.seed;
+  a.stream = 0;
+  a.ctr = 0;
+  HIPCHK(h, mdp_launch_eval(a, h->cfg.num_units, lds_eval_bytes(a.in, h->cfg.num_units), h->stream));
+  return 0;
+}
+
+int mdp_q_values(mdp_handle* h, int32_t agent, int32_t target, const float* x_dev, float* q_dev, int32_t rows) {
+  if (bad_agent(h, agent)) return -1;
+  if (rows <= 0) return 0;
+  const ADesc& ag = h->L.topo.ag[agent];
+  EvalArgs a;
+  a.P = target ? h->target : h->theta;
+  a.net = ag.critic;
+  a.in = ag.cin;
+  a.rows = rows;
+  a.x = x_dev;
+  a.out = q_dev;
+  a.gumbel = 0;
+  a.u = nullptr;
+  a.seed = h->cfg.seed;
+  a.stream = 0;
+  a.ctr = 0;
+  HIPCHK(h, mdp_launch_eval(a, h->cfg.num_units, lds_eval_bytes(a.in, h->cfg.num_units), h->stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------- training
+int mdp_update_gate(mdp_handle* h, int64_t t) {
+  if (h->len < (int64_t)h->cfg.batch_size * h->cfg.max_episode_len) return 1;  // maddpg.py:162-163
+  if (t % 100 != 0) return 1;                                                   // maddpg.py:164-165
+  return 0;
+}
+
+int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev, const float* u_act_dev) {
+  if (bad_agent(h, agent)) return -1;
+  const int32_t* idx = idx_dev;
+  if (!idx) {
+    int32_t* slot = h->index + (int64_t)agent * h->cfg.batch_size;
+    int rc = launch_make_index(h, h->cfg.batch_size, slot);
+    if (rc) return rc;
+    idx = slot;
+  }
+  return do_update(h, agent, idx, u_tgt_dev, u_act_dev);
+}
+
+int mdp_update_round(mdp_handle* h) {
+  const int n = h->cfg.n_agents, B = h->cfg.batch_size;
+  int rc = launch_make_index(h, n * B, h->index);
+  if (rc) return rc;
+  for (int i = 0; i < n; ++i)
+    if ((rc = do_update(h, i, h->index + (int64_t)i * B, nullptr, nullptr))) return rc;
+  return 0;
+}
+
+int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev) {
+  if (bad_agent(h, agent)) return -1;
+  if (!idx_dev) return fail(h, "critic_grad needs indices");
+  return do_critic_grad(h, agent, idx_dev, u_tgt_dev);
+}
+
+int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev) {
+  if (bad_agent(h, agent)) return -1;
+  if (!idx_dev) return fail(h, "actor_grad needs indices");
+  return do_actor_grad(h, agent, idx_dev, u_act_dev);
+}
+
+int mdp_reduce_grad(mdp_handle* h, int32_t agent, int32_t net) {
+  if (bad_agent(h, agent)) return -1;
+  const NDesc& d = net_of(h, agent, net);
+  ReduceArgs a;
+  a.slab = net ? h->slab_c : h->slab_a;
+  a.nwg = h->L.nwg;
+  a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
+  a.grad = h->grad;
+  a.off = d.off;
+  a.size = d.size;
+  ProfScope p(h, MDP_K_REDUCE);
+  HIPCHK(h, mdp_launch_reduce(a, h->stream));
+  return 0;
+}
+
+int mdp_apply_grad(mdp_handle* h, int32_t agent, int32_t net, float scale) {
+  if (bad_agent(h, agent)) return -1;
+  return do_apply(h, agent, net ? 1 : 0, false, scale);
+}
+
+int mdp_get_stats(mdp_handle* h, int32_t agent, double out6[6]) {
+  if (bad_agent(h, agent)) return -1;
+  double buf[8];
+  HIPCHK(h, hipMemcpyAsync(buf, h->stats + agent * 8, sizeof(buf), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (int i = 0; i < 6; ++i) out6[i] = buf[i];
+  return 0;
+}
+
+// -------------------------------------------------------------------- env
+static int need_env(mdp_handle* h) {
+  if (h->cfg.scenario == MDP_SCN_NONE || h->cfg.num_envs <= 0) return fail(h, "handle has no device env");
+  return 0;
+}
+
+int mdp_env_reset(mdp_handle* h) {
+  if (need_env(h)) return -1;
+  EnvResetArgs a;
+  a.env = h->L.env;
+  a.seed = h->cfg.seed;
+  a.ctr = h->reset_ctr++;
+  a.env_base = h->cfg.rank * h->cfg.num_envs;
+  a.E = h->cfg.num_envs;
+  a.pos = h->pos;
+  a.vel = h->vel;
+  a.goal = h->goal;
+  a.ep_step = h->ep_step;
+  a.ep_rew = h->ep_rew;
+  HIPCHK(h, mdp_launch_env_reset(a, h->stream));
+  return 0;
+}
+
+int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
+  if (need_env(h)) return -1;
+  RolloutArgs a;
+  a.topo = h->L.topo;
+  a.env = h->L.env;
+  a.theta = h->theta;
+  a.replay = h->replay;
+  a.cap = h->cfg.capacity;
+  a.pos = h->pos;
+  a.vel = h->vel;
+  a.goal = h->goal;
+  a.ep_step = h->ep_step;
+  a.ep_rew = h->ep_rew;
+  a.eplog = h->eplog;
+  a.eplog_cap = h->L.eplog_rows;
+  a.ctl = h->ctl;
+  a.seed = h->cfg.seed;
+  a.E = h->cfg.num_envs;
+  a.env_base = h->cfg.rank * h->cfg.num_envs;
+  a.act_in = act_in_dev;
+  a.u_in = u_dev;
+  a.ticket = &h->ctl->ticket[2];
+  {
+    ProfScope p(h, MDP_K_ROLLOUT);
+    HIPCHK(h, mdp_launch_rollout(a, h->cfg.num_units, lds_rollout_bytes(h->L.topo), h->stream));
+  }
+  const int64_t cap = h->cfg.capacity, E = h->cfg.num_envs;
+  h->len = std::min(cap, h->len + E);
+  h->next = (h->next + E) % cap;
+  return 0;
+}
+
+int mdp_env_get_state(mdp_handle* h, float* pos, float* vel, int32_t* goal, int32_t* ep_step) {
+  if (need_env(h)) return -1;
+  const int64_t E = h->cfg.num_envs, ne = h->L.n_ent;
+  if (pos) HIPCHK(h, hipMemcpyAsync(pos, h->pos, 4 * E * ne * 2, hipMemcpyDeviceToHost, h->stream));
+  if (vel) HIPCHK(h, hipMemcpyAsync(vel, h->vel, 4 * E * ne * 2, hipMemcpyDeviceToHost, h->stream));
+  if (goal) HIPCHK(h, hipMemcpyAsync(goal, h->goal, 4 * E, hipMemcpyDeviceToHost, h->stream));
+  if (ep_step) HIPCHK(h, hipMemcpyAsync(ep_step, h->ep_step, 4 * E, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_env_set_state(mdp_handle* h, const float* pos, const float* vel, const int32_t* goal, const int32_t* ep_step) {
+  if (need_env(h)) return -1;
+  const int64_t E = h->cfg.num_envs, ne = h->L.n_ent;
+  if (pos) HIPCHK(h, hipMemcpyAsync(h->pos, pos, 4 * E * ne * 2, hipMemcpyHostToDevice, h->stream));
+  if (vel) HIPCHK(h, hipMemcpyAsync(h->vel, vel, 4 * E * ne * 2, hipMemcpyHostToDevice, h->stream));
+  if (goal) HIPCHK(h, hipMemcpyAsync(h->goal, goal, 4 * E, hipMemcpyHostToDevice, h->stream));
+  if (ep_step) HIPCHK(h, hipMemcpyAsync(h->ep_step, ep_step, 4 * E, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int mdp_env_obs(mdp_handle* h, float* obs_dev) {
+  if (need_env(h)) return -1;
+  EnvObsArgs a;
+  a.topo = h->L.topo;
+  a.env = h->L.env;
+  a.E = h->cfg.num_envs;
+  a.pos = h->pos;
+  a.vel = h->vel;
+  a.goal = h->goal;
+  a.obs = obs_dev;
+  HIPCHK(h, mdp_launch_env_obs(a, h->stream));
+  return 0;
+}
+
+int64_t mdp_episode_count(mdp_handle* h) {
+  int64_t n = 0;
+  if (hipMemcpyAsync(&n, &h->ctl->episodes, 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess) return -1;
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return -1;
+  return n;
+}
+
+int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out) {
+  const int64_t cap = h->L.eplog_rows, w = 1 + h->cfg.n_agents;
+  if (n > cap) return fail(h, "episode log request exceeds ring");
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t slot = (first + k) % cap;
+    HIPCHK(h, hipMemcpyAsync(out + k * w, h->eplog + slot * w, 4 * w, hipMemcpyDeviceToHost, h->stream));
+  }
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// -------------------------------------------------------------- profiling
+int mdp_prof_enable(mdp_handle* h, int32_t kind, int32_t on) {
+  if (kind < 0 || kind >= MDP_K_COUNT) return fail(h, "bad kernel kind");
+  if (!on) flush_prof(h, kind);
+  h->prof_on[kind] = on != 0;
+  if (on) {
+    h->prof_ms[kind] = 0.0;
+    h->prof_n[kind] = 0;
+    h->ev_used[kind] = 0;
+  }
+  return 0;
+}
+
+int mdp_prof_read(mdp_handle* h, int32_t kind, double* total_ms, int64_t* launches) {
+  if (kind < 0 || kind >= MDP_K_COUNT) return fail(h, "bad kernel kind");
+  flush_prof(h, kind);
+  if (total_ms) *total_ms = h->prof_ms[kind];
+  if (launches) *launches = h->prof_n[kind];
+  return 0;
+}
+
+}  // extern "C"

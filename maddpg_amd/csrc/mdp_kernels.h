@@ -1,0 +1,163 @@
+// mdp_kernels.h -- kernel argument blocks and host-side launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mdp_topo.h"
+
+struct CriticArgs {
+  Topo topo;
+  int agent, B;
+  const float* theta;
+  const float* target;
+  const float* replay;
+  const int32_t* idx;
+  const float* u_tgt;   // [n][B][5] or null
+  uint64_t seed;
+  const Ctl* ctl;
+  double gamma;
+  float inv_b;
+  float* slab;          // [nwg][slab_stride] partial critic grads (net-relative)
+  int slab_stride;
+  double* slab_stat;    // [nwg][8]
+  double* y_out;        // [B]
+};
+
+struct ActorArgs {
+  Topo topo;
+  int agent, B;
+  const float* theta;
+  const float* replay;
+  const int32_t* idx;
+  const float* u_act;   // [B][5] or null
+  uint64_t seed;
+  const Ctl* ctl;
+  float neg_inv_b;      // dL/dq = -1/B
+  float reg_scale;      // 2 * actor_reg / (B * 5)
+  float* slab;
+  int slab_stride;
+  double* slab_stat;
+};
+
+struct ReduceArgs {
+  const float* slab;
+  int nwg, slab_stride;
+  float* grad;
+  int64_t off, size;
+};
+
+struct ApplyArgs {
+  NDesc net, other;
+  float* theta;
+  float* target;
+  float* m;
+  float* v;
+  float* grad;
+  const float* slab;    // null: read grad[] (already reduced / all-reduced)
+  int slab_stride, nwg;
+  float scale, clip, lr, b1, b2, eps;
+  float* beta;          // [2] beta1^t, beta2^t of this optimizer
+  int polyak;
+  float pa, pb;         // fp32(1 - tau), fp32(1 - (1 - tau))
+  int stats_mode;       // 0 none, 1 critic, 2 actor
+  const double* slab_stat;
+  const double* y;
+  int B;
+  float reg;
+  double* stats_out;
+  uint32_t* ticket;
+  Ctl* ctl;
+  int bump_ctr;
+};
+
+struct RolloutArgs {
+  Topo topo;
+  EnvDesc env;
+  const float* theta;
+  float* replay;
+  int64_t cap;
+  float* pos;
+  float* vel;
+  int32_t* goal;
+  int32_t* ep_step;
+  float* ep_rew;
+  float* eplog;
+  int64_t eplog_cap;
+  Ctl* ctl;
+  uint64_t seed;
+  int E, env_base;
+  const float* act_in;
+  const float* u_in;
+  uint32_t* ticket;
+};
+
+struct EnvResetArgs {
+  EnvDesc env;
+  uint64_t seed;
+  uint32_t ctr;
+  int env_base, E;
+  float* pos;
+  float* vel;
+  int32_t* goal;
+  int32_t* ep_step;
+  float* ep_rew;
+};
+
+struct EnvObsArgs {
+  Topo topo;
+  EnvDesc env;
+  int E;
+  const float* pos;
+  const float* vel;
+  const int32_t* goal;
+  float* obs;
+};
+
+struct EvalArgs {
+  const float* P;
+  NDesc net;
+  int in, rows;
+  const float* x;
+  float* out;
+  int gumbel;
+  const float* u;
+  uint64_t seed;
+  uint32_t stream, ctr;
+};
+
+// ---- dynamic LDS sizes (must mirror the LdsCarve order in the kernels)
+inline int mdp_r4(int n) { return (n + 3) & ~3; }
+inline int mdp_ld(int c) { return c | 1; }
+inline int lds_critic_bytes(const Topo& t) {
+  const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), ldh = t.H + 1;
+  return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldc) + 6 * mdp_r4(R * ldh) + mdp_r4(R * 8) + 3 * mdp_r4(R) + 8);
+}
+inline int lds_actor_bytes(const Topo& t) {
+  const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), ldh = t.H + 1;
+  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(R * ldh) + 4 * mdp_r4(R * 8) + mdp_r4(R) + 8);
+}
+inline int lds_rollout_bytes(const Topo& t) {
+  const int R = 16, ldr = mdp_ld(t.row_stride), ldh = t.H + 1;
+  return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8) + 2 * mdp_r4(R * 2 * MDP_MAX_ENT));
+}
+inline int lds_eval_bytes(int in, int H) {
+  const int R = 16, ldx = mdp_ld(in), ldh = H + 1;
+  return 4 * (mdp_r4(R * ldx) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8));
+}
+
+hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
+hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s);
+hipError_t mdp_launch_rollout(const RolloutArgs& a, int H, int lds_bytes, hipStream_t s);
+hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t s);
+hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s);
+hipError_t mdp_launch_reduce(const ReduceArgs& a, hipStream_t s);
+hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t s);
+hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
+                             hipStream_t s);
+hipError_t mdp_launch_put_rows(float* replay, int stride, int64_t cap, int64_t next, const float* src, int64_t rows,
+                               hipStream_t s);
+hipError_t mdp_launch_put_agent(float* replay, int stride, const ADesc& ag, const int64_t* pos, const float* cols,
+                                int64_t rows, hipStream_t s);
+hipError_t mdp_launch_env_reset(const EnvResetArgs& a, hipStream_t s);
+hipError_t mdp_launch_env_obs(const EnvObsArgs& a, hipStream_t s);
+hipError_t mdp_launch_set_ring(Ctl* ctl, int64_t len, int64_t next, hipStream_t s);

@@ -1,0 +1,1214 @@
+// mdp_kernels.hip -- HIP kernels of the MADDPG hot path for gfx950 (MI355X).
+//
+// Kernel map (reference site -> kernel):
+//   replay_buffer.py:46-47  make_index        -> k_make_index   (CPython MT19937, 1 workgroup)
+//   replay_buffer.py:34-44  _encode_sample    -> k_gather_rows  (+ fused into the grad kernels)
+//   replay_buffer.py:25-32  add               -> k_put_rows / k_put_agent (+ fused into k_rollout)
+//   maddpg.py:184-188       target_act + target_q + TD + q_train grads -> k_critic_grad
+//   maddpg.py:46-61         p_train grads (through the critic's a_i input) -> k_actor_grad
+//   tf_util.py:177-182 + TF ApplyAdam + maddpg.py:20-26 -> k_apply (clip, Adam, Polyak)
+//   train.py:112-128 + MPE World.step -> k_rollout (actors + Gumbel + physics + obs/reward
+//                                        + replay append + episode reset), k_env_reset
+#include "mdp_device.h"
+#include "mdp_kernels.h"
+
+// ================================================================ index
+namespace {
+
+__device__ inline uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+__device__ inline uint32_t mt_mix(uint32_t cur, uint32_t nxt) {
+  const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+  return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// MT19937 generation step over 624 words in LDS, in 4 dependency stages.
+// Sequential form: for kk in 0..623: mt[kk] = mt[(kk+397)%624] ^ mix(mt[kk], mt[kk+1])
+// kk <  227 reads old mt[kk+397]; 227 <= kk < 623 reads new mt[kk-227]; kk = 623
+// reads new mt[396] and new mt[0].
+__device__ void mt_twist(uint32_t* mt) {
+  const int t = threadIdx.x;
+  uint32_t cur = 0, nxt = 0, far = 0;
+  if (t < 624) {
+    cur = mt[t];
+    nxt = mt[t + 1 < 624 ? t + 1 : 0];
+  }
+  if (t < 227) far = mt[t + 397];
+  __syncthreads();
+  if (t < 227) mt[t] = far ^ mt_mix(cur, nxt);
+  __syncthreads();
+  if (t >= 227 && t < 454) mt[t] = mt[t - 227] ^ mt_mix(cur, nxt);
+  __syncthreads();
+  if (t >= 454 && t < 623) mt[t] = mt[t - 227] ^ mt_mix(cur, nxt);
+  __syncthreads();
+  if (t == 623) mt[623] = mt[396] ^ mt_mix(cur, mt[0]);
+  __syncthreads();
+}
+
+}  // namespace
+
+// count x randint(0, len-1): r = getrandbits(k) = temper(next) >> (32-k),
+// k = len.bit_length(), rejected while r >= len (Lib/random.py _randbelow).
+// Accepted draws are compacted with a workgroup prefix sum; the stream
+// position after the count-th accepted draw is stored back.
+__global__ __launch_bounds__(1024) void k_make_index(Ctl* ctl, int count, int32_t* __restrict__ out) {
+  __shared__ uint32_t mt[624];
+  __shared__ int wsum[16];
+  __shared__ int s_newpos;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int i = t; i < 624; i += blockDim.x) mt[i] = ctl->mt[i];
+  int pos = ctl->mt_pos;
+  const uint32_t n = (uint32_t)ctl->len;
+  if (n == 0) {  // randint(0, -1) raises in the reference; the host refuses it too
+    for (int i = t; i < count; i += blockDim.x) out[i] = 0;
+    return;
+  }
+  const int k = 32 - __clz(n);
+  __syncthreads();
+  int produced = 0;
+  // acceptance >= 1/2 per draw, so ~count/312 passes; the bound only guards a hang
+  const int max_iters = 64 + count / 64;
+  int iters = 0;
+  while (produced < count && iters++ < max_iters) {
+    if (pos >= 624) {
+      mt_twist(mt);
+      pos = 0;
+    }
+    const int avail = 624 - pos;
+    bool acc = false;
+    uint32_t r = 0;
+    if (t < avail) {
+      r = mt_temper(mt[pos + t]) >> (32 - k);
+      acc = r < n;
+    }
+    const unsigned long long bal = __ballot(acc);
+    const int wrank = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int i = 0; i < 16; ++i) {
+      const int c = wsum[i];
+      before += (i < w) ? c : 0;
+      total += c;
+    }
+    const int rank = before + wrank;
+    const int need = count - produced;
+    if (acc && rank < need) out[produced + rank] = (int32_t)r;
+    if (total >= need) {
+      if (acc && rank == need - 1) s_newpos = pos + t + 1;
+      __syncthreads();
+      pos = s_newpos;
+      produced = count;
+    } else {
+      produced += total;
+      pos = 624;
+    }
+    __syncthreads();
+  }
+  for (int i = t; i < 624; i += blockDim.x) ctl->mt[i] = mt[i];
+  if (t == 0) ctl->mt_pos = pos;
+}
+
+// ================================================================ replay
+// out[b][:] = replay[idx[b]][:]   (one float4 per thread, rows contiguous)
+__global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ replay, int stride,
+                                                     const int32_t* __restrict__ idx, int count,
+                                                     float* __restrict__ out) {
+  const int v4 = stride >> 2;
+  const int64_t total = (int64_t)count * v4;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = e / v4;
+    const int c = (int)(e - b * v4);
+    const float4 v = *reinterpret_cast<const float4*>(replay + (int64_t)idx[b] * stride + c * 4);
+    *reinterpret_cast<float4*>(out + b * stride + c * 4) = v;
+  }
+}
+
+// ring append of whole rows: replay[(next + r) % cap] = src[r]
+__global__ __launch_bounds__(256) void k_put_rows(float* __restrict__ replay, int stride, int64_t cap,
+                                                  int64_t next, const float* __restrict__ src, int64_t rows) {
+  const int v4 = stride >> 2;
+  const int64_t total = rows * v4;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / v4;
+    const int c = (int)(e - r * v4);
+    const int64_t dst = (next + r) % cap;
+    *reinterpret_cast<float4*>(replay + dst * stride + c * 4) =
+        *reinterpret_cast<const float4*>(src + r * stride + c * 4);
+  }
+}
+
+// per-agent add (facade): cols = [obs(o) | act(5) | obs'(o) | rew | done] written at pos[r]
+__global__ __launch_bounds__(256) void k_put_agent(float* __restrict__ replay, int stride, int obs_off,
+                                                   int act_off, int nobs_off, int rew_off, int done_off,
+                                                   int o, const int64_t* __restrict__ pos,
+                                                   const float* __restrict__ cols, int64_t rows) {
+  const int w = 2 * o + MDP_ACT_DIM + 2;
+  const int64_t total = rows * w;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / w;
+    const int c = (int)(e - r * w);
+    int dc;
+    if (c < o) dc = obs_off + c;
+    else if (c < o + MDP_ACT_DIM) dc = act_off + (c - o);
+    else if (c < 2 * o + MDP_ACT_DIM) dc = nobs_off + (c - o - MDP_ACT_DIM);
+    else if (c == 2 * o + MDP_ACT_DIM) dc = rew_off;
+    else dc = done_off;
+    replay[pos[r] * stride + dc] = cols[e];
+  }
+}
+
+// ================================================================ grads
+namespace {
+
+__device__ inline void gather_tile(const float* __restrict__ replay, int stride, const int32_t* __restrict__ idx,
+                                   int r0, int nvalid, float* rowbuf, int ldr) {
+  const int v4 = stride >> 2;
+  for (int e = threadIdx.x; e < MDP_R * v4; e += MDP_NT) {
+    const int r = e / v4, c4 = e - r * v4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < nvalid) v = *reinterpret_cast<const float4*>(replay + (int64_t)idx[r0 + r] * stride + c4 * 4);
+    float* d = rowbuf + r * ldr + c4 * 4;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+}
+
+// copy ncols columns of a 16-row LDS tile
+__device__ inline void copy_cols(const float* src, int lds_src, int src_off, float* dst, int lds_dst, int dst_off,
+                                 int ncols) {
+  for (int e = threadIdx.x; e < MDP_R * ncols; e += MDP_NT) {
+    const int r = e / ncols, c = e - r * ncols;
+    dst[r * lds_dst + dst_off + c] = src[r * lds_src + src_off + c];
+  }
+}
+
+// column sums of a 16-row tile -> global
+__device__ inline void colsum_store(const float* X, int ldx, int ncols, float* __restrict__ out) {
+  for (int c = threadIdx.x; c < ncols; c += MDP_NT) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < MDP_R; ++r) s += X[r * ldx + c];
+    out[c] = s;
+  }
+}
+
+template <int H>
+__device__ inline void mlp_fwd_tile(const float* X, int ldx, int K, const float* P, const NDesc& nd, float* h1,
+                                    float* h2, int ldh, float* out, int ldo) {
+  tile_fwd<true>(X, ldx, K, P + nd.t[0].off, P + nd.t[1].off, H, h1, ldh);
+  __syncthreads();
+  tile_fwd<true>(h1, ldh, H, P + nd.t[2].off, P + nd.t[3].off, H, h2, ldh);
+  __syncthreads();
+  tile_head(h2, ldh, H, P + nd.t[4].off, P + nd.t[5].off, nd.out, out, ldo);
+  __syncthreads();
+}
+
+}  // namespace
+
+// One agent's critic step inputs and gradients (maddpg.py:180-188):
+// target actors of every agent on obs' (+ Gumbel), target critic, TD target
+// in fp64, critic forward, loss partials and per-workgroup critic gradients.
+template <int H>
+__global__ __launch_bounds__(MDP_NT) void k_critic_grad(CriticArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Topo& T = a.topo;
+  const ADesc& ag = T.ag[a.agent];
+  const int ldr = lds_ld(T.row_stride), ldc = lds_ld(T.cin_max), ldh = H + 1;
+  LdsCarve cv(lds);
+  float* rowbuf = cv.take(MDP_R * ldr);
+  float* xt = cv.take(MDP_R * ldc);
+  float* xl = cv.take(MDP_R * ldc);
+  float* h1 = cv.take(MDP_R * ldh);
+  float* h2 = cv.take(MDP_R * ldh);
+  float* h1c = cv.take(MDP_R * ldh);
+  float* h2c = cv.take(MDP_R * ldh);
+  float* d2 = cv.take(MDP_R * ldh);
+  float* d1 = cv.take(MDP_R * ldh);
+  float* lg = cv.take(MDP_R * 8);
+  float* qt = cv.take(MDP_R);
+  float* qv = cv.take(MDP_R);
+  float* dq = cv.take(MDP_R);
+  double* red = reinterpret_cast<double*>(cv.take(2 * MDP_NW));
+
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * MDP_R;
+  const int nvalid = min(MDP_R, a.B - r0);
+  const bool lq = ag.local_q != 0;
+  const uint32_t ctr = a.ctl->upd_ctr;
+
+  gather_tile(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+  __syncthreads();
+
+  // target critic input: [obs'_all | a~_all] (global) or [obs'_i | a~_i] (local)
+  if (lq) copy_cols(rowbuf, ldr, ag.nobs_off, xt, ldc, 0, ag.obs_dim);
+  else copy_cols(rowbuf, ldr, T.ag[0].nobs_off, xt, ldc, 0, T.sum_obs);
+
+  for (int j = 0; j < T.n; ++j) {
+    if (lq && j != a.agent) continue;   // a local critic only consumes a~_i
+    const ADesc& aj = T.ag[j];
+    mlp_fwd_tile<H>(rowbuf + aj.nobs_off, ldr, aj.obs_dim, a.target, aj.actor, h1, h2, ldh, lg, 8);
+    if (tid < MDP_R) {
+      float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
+      const int row = r0 + tid;
+      if (a.u_tgt) {
+        for (int k = 0; k < MDP_ACT_DIM; ++k)
+          u[k] = tid < nvalid ? a.u_tgt[((int64_t)j * a.B + row) * MDP_ACT_DIM + k] : 0.5f;
+      } else {
+        uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)row, u);
+      }
+      gumbel_softmax5(lg + tid * 8, u, act);
+      const int dst = lq ? ag.obs_dim : T.sum_obs + MDP_ACT_DIM * j;
+      for (int k = 0; k < MDP_ACT_DIM; ++k) xt[tid * ldc + dst + k] = act[k];
+    }
+    __syncthreads();
+  }
+
+  // target critic -> Q'(o', a~)
+  mlp_fwd_tile<H>(xt, ldc, ag.cin, a.target, ag.critic, h1, h2, ldh, qt, 1);
+
+  // critic forward on (obs_n, act_n): the row's prefix (global) or [obs_i | act_i]
+  const float* X = rowbuf;
+  int ldX = ldr;
+  if (lq) {
+    copy_cols(rowbuf, ldr, ag.obs_off, xl, ldc, 0, ag.obs_dim);
+    copy_cols(rowbuf, ldr, ag.act_off, xl, ldc, ag.obs_dim, MDP_ACT_DIM);
+    __syncthreads();
+    X = xl;
+    ldX = ldc;
+  }
+  mlp_fwd_tile<H>(X, ldX, ag.cin, a.theta, ag.critic, h1c, h2c, ldh, qv, 1);
+
+  // TD target (fp64, maddpg.py:186), loss partials, dL/dq = 2(q - y)/B
+  double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;
+  if (tid < MDP_R) {
+    float g = 0.f;
+    if (tid < nvalid) {
+      const double rew = (double)rowbuf[tid * ldr + ag.rew_off];
+      const double done = (double)rowbuf[tid * ldr + ag.done_off];
+      const double qn = (double)qt[tid];
+      const double y64 = rew + a.gamma * (1.0 - done) * qn;
+      const float y = (float)y64;
+      const float diff = qv[tid] - y;
+      g = (2.0f * diff) * a.inv_b;
+      s_l = (double)diff * (double)diff;
+      s_y = y64;
+      s_r = rew;
+      s_q = qn;
+      a.y_out[r0 + tid] = y64;
+    }
+    dq[tid] = g;
+  }
+  s_l = block_sum_d(s_l, red);
+  s_y = block_sum_d(s_y, red);
+  s_r = block_sum_d(s_r, red);
+  s_q = block_sum_d(s_q, red);
+  if (tid == 0) {
+    double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+    st[0] = s_l;
+    st[1] = s_y;
+    st[2] = s_r;
+    st[3] = s_q;
+  }
+  __syncthreads();
+
+  // backward through the critic (tf.gradients of q_loss w.r.t. q_func vars)
+  const NDesc& nd = ag.critic;
+  const float* W3 = a.theta + nd.t[4].off;
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
+  if (tid < H) {
+    float s = 0.f;
+    for (int r = 0; r < MDP_R; ++r) s = fmaf(h2c[r * ldh + tid], dq[r], s);
+    slab[nd.t[4].off + tid] = s;
+  }
+  if (tid == 0) {
+    float s = 0.f;
+    for (int r = 0; r < MDP_R; ++r) s += dq[r];
+    slab[nd.t[5].off] = s;
+  }
+  for (int e = tid; e < MDP_R * H; e += MDP_NT) {
+    const int r = e / H, h = e - r * H;
+    d2[r * ldh + h] = h2c[r * ldh + h] > 0.f ? dq[r] * W3[h] : 0.f;
+  }
+  __syncthreads();
+  tile_wgrad(h1c, ldh, H, d2, ldh, H, slab + nd.t[2].off);
+  colsum_store(d2, ldh, H, slab + nd.t[3].off);
+  tile_dgrad_relu(d2, ldh, H, a.theta + nd.t[2].off, H, h1c, ldh, d1, ldh);
+  __syncthreads();
+  tile_wgrad(X, ldX, ag.cin, d1, ldh, H, slab + nd.t[0].off);
+  colsum_store(d1, ldh, H, slab + nd.t[1].off);
+}
+
+// One agent's actor step gradients (maddpg.py:37-58): actor forward, fresh
+// Gumbel sample, critic (already updated) on the batch with a_i replaced,
+// backprop through the critic's a_i input slice, the softmax and the actor.
+template <int H>
+__global__ __launch_bounds__(MDP_NT) void k_actor_grad(ActorArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Topo& T = a.topo;
+  const ADesc& ag = T.ag[a.agent];
+  const int ldr = lds_ld(T.row_stride), ldc = lds_ld(T.cin_max), ldh = H + 1;
+  LdsCarve cv(lds);
+  float* rowbuf = cv.take(MDP_R * ldr);
+  float* x = cv.take(MDP_R * ldc);
+  float* h1a = cv.take(MDP_R * ldh);
+  float* h2a = cv.take(MDP_R * ldh);
+  float* h1c = cv.take(MDP_R * ldh);
+  float* h2c = cv.take(MDP_R * ldh);
+  float* d2 = cv.take(MDP_R * ldh);
+  float* d1 = cv.take(MDP_R * ldh);
+  float* lg = cv.take(MDP_R * 8);
+  float* av = cv.take(MDP_R * 8);
+  float* da = cv.take(MDP_R * 8);
+  float* dl = cv.take(MDP_R * 8);
+  float* qv = cv.take(MDP_R);
+  double* red = reinterpret_cast<double*>(cv.take(2 * MDP_NW));
+
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * MDP_R;
+  const int nvalid = min(MDP_R, a.B - r0);
+  const bool lq = ag.local_q != 0;
+  const uint32_t ctr = a.ctl->upd_ctr;
+  const NDesc& na = ag.actor;
+  const NDesc& nc = ag.critic;
+
+  gather_tile(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+  __syncthreads();
+
+  // actor forward on obs_i -> logits p (maddpg.py:39)
+  mlp_fwd_tile<H>(rowbuf + ag.obs_off, ldr, ag.obs_dim, a.theta, na, h1a, h2a, ldh, lg, 8);
+  if (tid < MDP_R) {
+    float u[MDP_ACT_DIM];
+    const int row = r0 + tid;
+    if (a.u_act) {
+      for (int k = 0; k < MDP_ACT_DIM; ++k)
+        u[k] = tid < nvalid ? a.u_act[(int64_t)row * MDP_ACT_DIM + k] : 0.5f;
+    } else {
+      uniforms5(a.seed, (uint32_t)((a.agent << 8) | 0x80), ctr, (uint32_t)row, u);
+    }
+    gumbel_softmax5(lg + tid * 8, u, av + tid * 8);
+  }
+  // critic input with act_input_n[i] = gumbel sample (maddpg.py:48-52)
+  if (lq) {
+    copy_cols(rowbuf, ldr, ag.obs_off, x, ldc, 0, ag.obs_dim);
+  } else {
+    copy_cols(rowbuf, ldr, 0, x, ldc, 0, ag.cin);
+  }
+  __syncthreads();
+  if (tid < MDP_R) {
+    for (int k = 0; k < MDP_ACT_DIM; ++k) x[tid * ldc + ag.a_in_off + k] = av[tid * 8 + k];
+  }
+  __syncthreads();
+  mlp_fwd_tile<H>(x, ldc, ag.cin, a.theta, nc, h1c, h2c, ldh, qv, 1);
+
+  // loss partials: -mean(q) + reg * mean(p^2)
+  double s_q = 0.0, s_p = 0.0;
+  if (tid < nvalid) {
+    s_q = (double)qv[tid];
+    for (int k = 0; k < MDP_ACT_DIM; ++k) {
+      const double p = (double)lg[tid * 8 + k];
+      s_p += p * p;
+    }
+  }
+  s_q = block_sum_d(s_q, red);
+  s_p = block_sum_d(s_p, red);
+  if (tid == 0) {
+    double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+    st[0] = s_q;
+    st[1] = s_p;
+  }
+
+  // dL/dq = -1/B ; back through critic layers 3, 2 to h1
+  const float* W3c = a.theta + nc.t[4].off;
+  for (int e = tid; e < MDP_R * H; e += MDP_NT) {
+    const int r = e / H, h = e - r * H;
+    d2[r * ldh + h] = (r < nvalid && h2c[r * ldh + h] > 0.f) ? a.neg_inv_b * W3c[h] : 0.f;
+  }
+  __syncthreads();
+  tile_dgrad_relu(d2, ldh, H, a.theta + nc.t[2].off, H, h1c, ldh, d1, ldh);
+  __syncthreads();
+  // da[r][k] = sum_h d1[r][h] * W1c[a_in_off + k][h]   (only the a_i input columns)
+  {
+    const float* W1c = a.theta + nc.t[0].off + (int64_t)ag.a_in_off * H;
+    for (int base = 0; base < MDP_R * MDP_ACT_DIM * 4; base += MDP_NT) {
+      const int t = base + tid;
+      const int o = t >> 2, q = t & 3;
+      float s = 0.f;
+      if (o < MDP_R * MDP_ACT_DIM) {
+        const int r = o / MDP_ACT_DIM, k = o - r * MDP_ACT_DIM;
+        for (int h = q; h < H; h += 4) s = fmaf(d1[r * ldh + h], W1c[k * H + h], s);
+      }
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      if (o < MDP_R * MDP_ACT_DIM && q == 0) {
+        const int r = o / MDP_ACT_DIM, k = o - r * MDP_ACT_DIM;
+        da[r * 8 + k] = s;
+      }
+    }
+  }
+  __syncthreads();
+  // softmax backward + regulariser: dlogits = (da - sum(a*da)) * a + reg*2*p/(B*A)
+  if (tid < MDP_R) {
+    float dot = 0.f;
+    for (int k = 0; k < MDP_ACT_DIM; ++k) dot += da[tid * 8 + k] * av[tid * 8 + k];
+    for (int k = 0; k < MDP_ACT_DIM; ++k) {
+      const float g = (da[tid * 8 + k] - dot) * av[tid * 8 + k] + lg[tid * 8 + k] * a.reg_scale;
+      dl[tid * 8 + k] = tid < nvalid ? g : 0.f;
+    }
+  }
+  __syncthreads();
+
+  // actor backward
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
+  const float* W3a = a.theta + na.t[4].off;
+  for (int e = tid; e < H * MDP_ACT_DIM; e += MDP_NT) {
+    const int h = e / MDP_ACT_DIM, k = e - h * MDP_ACT_DIM;
+    float s = 0.f;
+    for (int r = 0; r < MDP_R; ++r) s = fmaf(h2a[r * ldh + h], dl[r * 8 + k], s);
+    slab[na.t[4].off + e] = s;
+  }
+  if (tid < MDP_ACT_DIM) {
+    float s = 0.f;
+    for (int r = 0; r < MDP_R; ++r) s += dl[r * 8 + tid];
+    slab[na.t[5].off + tid] = s;
+  }
+  for (int e = tid; e < MDP_R * H; e += MDP_NT) {
+    const int r = e / H, h = e - r * H;
+    float s = 0.f;
+    for (int k = 0; k < MDP_ACT_DIM; ++k) s = fmaf(dl[r * 8 + k], W3a[h * MDP_ACT_DIM + k], s);
+    d2[r * ldh + h] = h2a[r * ldh + h] > 0.f ? s : 0.f;
+  }
+  __syncthreads();
+  tile_wgrad(h1a, ldh, H, d2, ldh, H, slab + na.t[2].off);
+  colsum_store(d2, ldh, H, slab + na.t[3].off);
+  tile_dgrad_relu(d2, ldh, H, a.theta + na.t[2].off, H, h1a, ldh, d1, ldh);
+  __syncthreads();
+  tile_wgrad(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1, ldh, H, slab + na.t[0].off);
+  colsum_store(d1, ldh, H, slab + na.t[1].off);
+}
+
+// ================================================================ apply
+namespace {
+// true in every thread of the last workgroup to arrive (no static LDS: keeps
+// the dynamic LDS base 16-B aligned)
+__device__ inline bool last_block(uint32_t* ticket) {
+  int last = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t old = atomicAdd(ticket, 1u);
+    last = (old == gridDim.x - 1) ? 1 : 0;
+  }
+  return __syncthreads_or(last) != 0;
+}
+}  // namespace
+
+// Reduce per-workgroup partials of one net into grad[] (fixed order -> deterministic).
+__global__ __launch_bounds__(256) void k_reduce(ReduceArgs a) {
+  const int64_t n = a.size;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int w = 0; w < a.nwg; ++w) s += a.slab[(int64_t)w * a.slab_stride + e];
+    a.grad[a.off + e] = s;
+  }
+}
+
+// blocks 0..5: tensor b of `net`: reduce partials (or read grad), scale,
+// per-tensor clip_by_norm, TF1 ApplyAdam, optional Polyak of that tensor;
+// blocks 6..11 (polyak): Polyak of `other`'s tensors; last block: stats.
+// The last block to finish also advances this optimizer's beta powers.
+__global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float b1p = a.beta[0], b2p = a.beta[1];
+  if (b < 6) {
+    const TDesc td = a.net.t[b];
+    const int n = td.rows * td.cols;
+    const int rel = td.off - a.net.off;
+    double ss = 0.0;
+    for (int e = tid; e < n; e += blockDim.x) {
+      float g;
+      if (a.slab) {
+        g = 0.f;
+        for (int w = 0; w < a.nwg; ++w) g += a.slab[(int64_t)w * a.slab_stride + rel + e];
+      } else {
+        g = a.grad[td.off + e];
+      }
+      g = g * a.scale;
+      a.grad[td.off + e] = g;
+      ss += (double)g * (double)g;
+    }
+    ss = block_sum_d(ss, red);
+    const float norm = (float)sqrt(ss);
+    const float clip = a.clip;
+    const float denom = fmaxf(norm, clip);
+    const float one = 1.0f;
+    const float alpha = a.lr * sqrtf(one - b2p) / (one - b1p);
+    const float c1 = one - a.b1, c2 = one - a.b2;
+    for (int e = tid; e < n; e += blockDim.x) {
+      const int64_t i = td.off + e;
+      const float g = (a.grad[i] * clip) / denom;
+      const float m = a.m[i] + (g - a.m[i]) * c1;
+      const float v = a.v[i] + (g * g - a.v[i]) * c2;
+      const float th = a.theta[i] - (m * alpha) / (sqrtf(v) + a.eps);
+      a.m[i] = m;
+      a.v[i] = v;
+      a.theta[i] = th;
+      if (a.polyak) a.target[i] = a.pa * a.target[i] + a.pb * th;
+    }
+  } else if (a.polyak && b < 12) {
+    const TDesc td = a.other.t[b - 6];
+    const int n = td.rows * td.cols;
+    for (int e = tid; e < n; e += blockDim.x) {
+      const int64_t i = td.off + e;
+      a.target[i] = a.pa * a.target[i] + a.pb * a.theta[i];
+    }
+  } else if (a.stats_mode) {
+    // stats block (maddpg.py:196): critic fills 0,2,3,4,5; actor fills 1
+    if (a.stats_mode == 1) {
+      double sl = 0.0, sy = 0.0, sr = 0.0, sq = 0.0;
+      if (tid == 0) {
+        for (int w = 0; w < a.nwg; ++w) {
+          const double* st = a.slab_stat + (int64_t)w * 8;
+          sl += st[0];
+          sy += st[1];
+          sr += st[2];
+          sq += st[3];
+        }
+        red[0] = sy / a.B;
+      }
+      __syncthreads();
+      const double mean_y = red[0];
+      double dv = 0.0;
+      for (int i = tid; i < a.B; i += blockDim.x) {
+        const double d = a.y[i] - mean_y;
+        dv += d * d;
+      }
+      __syncthreads();
+      dv = block_sum_d(dv, red);
+      if (tid == 0) {
+        a.stats_out[0] = sl / a.B;
+        a.stats_out[2] = mean_y;
+        a.stats_out[3] = sr / a.B;
+        a.stats_out[4] = sq / a.B;
+        a.stats_out[5] = sqrt(dv / a.B);
+      }
+    } else if (tid == 0) {
+      double sq = 0.0, sp = 0.0;
+      for (int w = 0; w < a.nwg; ++w) {
+        sq += a.slab_stat[(int64_t)w * 8 + 0];
+        sp += a.slab_stat[(int64_t)w * 8 + 1];
+      }
+      a.stats_out[1] = -sq / a.B + (double)a.reg * (sp / ((double)a.B * MDP_ACT_DIM));
+    }
+  }
+  if (last_block(a.ticket) && tid == 0) {
+    a.beta[0] = b1p * a.b1;
+    a.beta[1] = b2p * a.b2;
+    if (a.bump_ctr) a.ctl->upd_ctr += 1u;
+    *a.ticket = 0u;
+  }
+}
+
+// ================================================================ env
+namespace {
+
+struct EnvTile {
+  float* pos;  // [16][ne][2]
+  float* vel;
+};
+
+__device__ inline float softplus_f(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
+
+__device__ inline float dist2(const float* p, int a, int b) {
+  const float dx = p[2 * a] - p[2 * b], dy = p[2 * a + 1] - p[2 * b + 1];
+  return sqrtf(dx * dx + dy * dy);
+}
+
+// observation of agent i into o[] (scenario observation(), see oracle/mpe.py)
+__device__ inline void env_obs(const EnvDesc& E, const float* p, const float* v, int goal, int i, float* o) {
+  const int n = E.n_agents, L = E.n_landmarks;
+  int c = 0;
+  switch (E.scenario) {
+    case MDP_SCN_SIMPLE:
+      o[c++] = v[2 * i];
+      o[c++] = v[2 * i + 1];
+      for (int l = 0; l < L; ++l) {
+        o[c++] = p[2 * (n + l)] - p[2 * i];
+        o[c++] = p[2 * (n + l) + 1] - p[2 * i + 1];
+      }
+      break;
+    case MDP_SCN_SPREAD:
+      o[c++] = v[2 * i];
+      o[c++] = v[2 * i + 1];
+      o[c++] = p[2 * i];
+      o[c++] = p[2 * i + 1];
+      for (int l = 0; l < L; ++l) {
+        o[c++] = p[2 * (n + l)] - p[2 * i];
+        o[c++] = p[2 * (n + l) + 1] - p[2 * i + 1];
+      }
+      for (int j = 0; j < n; ++j) {
+        if (j == i) continue;
+        o[c++] = p[2 * j] - p[2 * i];
+        o[c++] = p[2 * j + 1] - p[2 * i + 1];
+      }
+      for (int j = 0; j < n; ++j) {
+        if (j == i) continue;
+        o[c++] = 0.f;  // other.state.c (silent agents)
+        o[c++] = 0.f;
+      }
+      break;
+    case MDP_SCN_ADVERSARY:
+      if (!E.adversary[i]) {
+        o[c++] = p[2 * (n + goal)] - p[2 * i];
+        o[c++] = p[2 * (n + goal) + 1] - p[2 * i + 1];
+      }
+      for (int l = 0; l < L; ++l) {
+        o[c++] = p[2 * (n + l)] - p[2 * i];
+        o[c++] = p[2 * (n + l) + 1] - p[2 * i + 1];
+      }
+      for (int j = 0; j < n; ++j) {
+        if (j == i) continue;
+        o[c++] = p[2 * j] - p[2 * i];
+        o[c++] = p[2 * j + 1] - p[2 * i + 1];
+      }
+      break;
+    case MDP_SCN_TAG:
+      o[c++] = v[2 * i];
+      o[c++] = v[2 * i + 1];
+      o[c++] = p[2 * i];
+      o[c++] = p[2 * i + 1];
+      for (int l = 0; l < L; ++l) {
+        o[c++] = p[2 * (n + l)] - p[2 * i];
+        o[c++] = p[2 * (n + l) + 1] - p[2 * i + 1];
+      }
+      for (int j = 0; j < n; ++j) {
+        if (j == i) continue;
+        o[c++] = p[2 * j] - p[2 * i];
+        o[c++] = p[2 * j + 1] - p[2 * i + 1];
+      }
+      for (int j = 0; j < n; ++j) {
+        if (j == i || E.adversary[j]) continue;
+        o[c++] = v[2 * j];
+        o[c++] = v[2 * j + 1];
+      }
+      break;
+    default:
+      break;
+  }
+}
+
+// rewards of all agents (scenario reward() + shared reward for collaborative worlds)
+__device__ inline void env_reward(const EnvDesc& E, const float* p, int goal, float* rew) {
+  const int n = E.n_agents, L = E.n_landmarks;
+  switch (E.scenario) {
+    case MDP_SCN_SIMPLE: {
+      const float dx = p[0] - p[2 * n], dy = p[1] - p[2 * n + 1];
+      rew[0] = -(dx * dx + dy * dy);
+      break;
+    }
+    case MDP_SCN_SPREAD: {
+      float base = 0.f;
+      for (int l = 0; l < L; ++l) {
+        float m = INFINITY;
+        for (int a = 0; a < n; ++a) m = fminf(m, dist2(p, a, n + l));
+        base -= m;
+      }
+      float tot = 0.f;
+      for (int i = 0; i < n; ++i) {
+        float r = base;
+        for (int a = 0; a < n; ++a)
+          if (dist2(p, a, i) < E.size[a] + E.size[i]) r -= 1.f;
+        tot += r;
+      }
+      for (int i = 0; i < n; ++i) rew[i] = tot;  // world.collaborative: reward_n = [sum] * n
+      break;
+    }
+    case MDP_SCN_ADVERSARY: {
+      const int g = n + goal;
+      float adv = 0.f, mg = INFINITY;
+      for (int a = 0; a < n; ++a) {
+        if (E.adversary[a]) adv += dist2(p, a, g);
+        else mg = fminf(mg, dist2(p, a, g));
+      }
+      for (int i = 0; i < n; ++i) {
+        if (E.adversary[i]) {
+          const float dx = p[2 * i] - p[2 * g], dy = p[2 * i + 1] - p[2 * g + 1];
+          rew[i] = -(dx * dx + dy * dy);
+        } else {
+          rew[i] = -mg + adv;
+        }
+      }
+      break;
+    }
+    case MDP_SCN_TAG: {
+      float caught = 0.f;
+      for (int g = 0; g < n; ++g) {
+        if (E.adversary[g]) continue;
+        for (int a = 0; a < n; ++a)
+          if (E.adversary[a] && dist2(p, g, a) < E.size[g] + E.size[a]) caught += 1.f;
+      }
+      for (int i = 0; i < n; ++i) {
+        if (E.adversary[i]) {
+          rew[i] = 10.f * caught;
+        } else {
+          float r = 0.f;
+          for (int a = 0; a < n; ++a)
+            if (E.adversary[a] && dist2(p, a, i) < E.size[a] + E.size[i]) r -= 10.f;
+          for (int d = 0; d < 2; ++d) {
+            const float x = fabsf(p[2 * i + d]);
+            float bnd = 0.f;
+            if (x < 0.9f) bnd = 0.f;
+            else if (x < 1.0f) bnd = (x - 0.9f) * 10.f;
+            else bnd = fminf(expf(2.f * x - 2.f), 10.f);
+            r -= bnd;
+          }
+          rew[i] = r;
+        }
+      }
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+// World.step (core.py): action force, pairwise soft contact, damping,
+// integration with max_speed clamp.  p, v: [ne][2] of one env (in place).
+__device__ inline void env_physics(const EnvDesc& E, float* p, float* v, const float* act /*[n][5]*/) {
+  const int n = E.n_agents, ne = E.n_agents + E.n_landmarks;
+  float fx[MDP_MAX_ENT], fy[MDP_MAX_ENT];
+  bool has[MDP_MAX_ENT];
+  for (int e = 0; e < ne; ++e) {
+    fx[e] = 0.f;
+    fy[e] = 0.f;
+    has[e] = false;
+  }
+  for (int i = 0; i < n; ++i) {  // environment._set_action, discrete action space
+    const float* a = act + i * MDP_ACT_DIM;
+    fx[i] = (a[1] - a[2]) * E.accel[i];
+    fy[i] = (a[3] - a[4]) * E.accel[i];
+    has[i] = true;
+  }
+  const float k = 1e-3f;  // contact_margin
+  for (int a = 0; a < ne; ++a) {
+    if (!E.collide[a]) continue;
+    for (int b = a + 1; b < ne; ++b) {
+      if (!E.collide[b]) continue;
+      const float dx = p[2 * a] - p[2 * b], dy = p[2 * a + 1] - p[2 * b + 1];
+      const float dist = sqrtf(dx * dx + dy * dy);
+      const float dmin = E.size[a] + E.size[b];
+      const float pen = softplus_f(-(dist - dmin) / k) * k;
+      const float sx = 1e2f * dx / dist * pen, sy = 1e2f * dy / dist * pen;
+      if (E.movable[a]) {
+        fx[a] = sx + fx[a];
+        fy[a] = sy + fy[a];
+        has[a] = true;
+      }
+      if (E.movable[b]) {
+        fx[b] = -sx + fx[b];
+        fy[b] = -sy + fy[b];
+        has[b] = true;
+      }
+    }
+  }
+  for (int e = 0; e < ne; ++e) {
+    if (!E.movable[e]) continue;
+    float vx = v[2 * e] * (1.f - 0.25f), vy = v[2 * e + 1] * (1.f - 0.25f);
+    if (has[e]) {
+      vx += (fx[e] / 1.f) * 0.1f;
+      vy += (fy[e] / 1.f) * 0.1f;
+    }
+    const float ms = E.max_speed[e];
+    if (ms >= 0.f) {
+      const float sp = sqrtf(vx * vx + vy * vy);
+      if (sp > ms) {
+        const float s = sqrtf(vx * vx + vy * vy);
+        vx = vx / s * ms;
+        vy = vy / s * ms;
+      }
+    }
+    v[2 * e] = vx;
+    v[2 * e + 1] = vy;
+    p[2 * e] += vx * 0.1f;
+    p[2 * e + 1] += vy * 0.1f;
+  }
+}
+
+// reset_world of one env from Philox uniforms
+__device__ inline void env_reset_one(const EnvDesc& E, uint64_t seed, uint32_t stream, uint32_t ctr, uint32_t env,
+                                     float* p, float* v, int32_t* goal) {
+  const int n = E.n_agents, ne = E.n_agents + E.n_landmarks;
+  uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  float u[4 * 5];
+  for (int q = 0; q < 5; ++q) {
+    const uint4 r = Philox::gen(make_uint4(env, ctr, stream, (uint32_t)q), key);
+    u[4 * q] = u01(r.x);
+    u[4 * q + 1] = u01(r.y);
+    u[4 * q + 2] = u01(r.z);
+    u[4 * q + 3] = u01(r.w);
+  }
+  int c = 0;
+  for (int e = 0; e < ne; ++e) {
+    float lo = -1.f, hi = 1.f, sc = 1.f;
+    if (e >= n) {
+      if (E.scenario == MDP_SCN_SPREAD || E.scenario == MDP_SCN_ADVERSARY) sc = 0.8f;
+      if (E.scenario == MDP_SCN_TAG) {
+        lo = -0.9f;
+        hi = 0.9f;
+      }
+    }
+    p[2 * e] = sc * (lo + (hi - lo) * u[c++]);
+    p[2 * e + 1] = sc * (lo + (hi - lo) * u[c++]);
+    v[2 * e] = 0.f;
+    v[2 * e + 1] = 0.f;
+  }
+  if (E.scenario == MDP_SCN_ADVERSARY) {
+    int g = (int)(u[c] * E.n_landmarks);
+    *goal = g < E.n_landmarks ? g : E.n_landmarks - 1;
+  } else {
+    *goal = 0;
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_env_reset(EnvResetArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.E) return;
+  const int ne = a.env.n_agents + a.env.n_landmarks;
+  float p[2 * MDP_MAX_ENT], v[2 * MDP_MAX_ENT];
+  int32_t g;
+  env_reset_one(a.env, a.seed, 0x30000u, a.ctr, (uint32_t)(a.env_base + e), p, v, &g);
+  for (int q = 0; q < 2 * ne; ++q) {
+    a.pos[(int64_t)e * 2 * ne + q] = p[q];
+    a.vel[(int64_t)e * 2 * ne + q] = v[q];
+  }
+  a.goal[e] = g;
+  a.ep_step[e] = 0;
+  for (int j = 0; j < a.env.n_agents; ++j) a.ep_rew[(int64_t)e * a.env.n_agents + j] = 0.f;
+}
+
+// current observations [E][sum_obs]
+__global__ __launch_bounds__(256) void k_env_obs(EnvObsArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.E) return;
+  const int ne = a.env.n_agents + a.env.n_landmarks;
+  const float* p = a.pos + (int64_t)e * 2 * ne;
+  const float* v = a.vel + (int64_t)e * 2 * ne;
+  float* o = a.obs + (int64_t)e * a.topo.sum_obs;
+  for (int j = 0; j < a.env.n_agents; ++j) env_obs(a.env, p, v, a.goal[e], j, o + a.topo.ag[j].obs_off);
+}
+
+// One vector env step for 16 env copies per workgroup (train.py:112-128).
+template <int H>
+__global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Topo& T = a.topo;
+  const EnvDesc& E = a.env;
+  const int n = E.n_agents, ne = E.n_agents + E.n_landmarks;
+  const int ldr = lds_ld(T.row_stride), ldh = H + 1;
+  LdsCarve cv(lds);
+  float* rowt = cv.take(MDP_R * ldr);
+  float* h1 = cv.take(MDP_R * ldh);
+  float* h2 = cv.take(MDP_R * ldh);
+  float* lg = cv.take(MDP_R * 8);
+  float* sp = cv.take(MDP_R * 2 * MDP_MAX_ENT);
+  float* sv = cv.take(MDP_R * 2 * MDP_MAX_ENT);
+
+  const int tid = threadIdx.x;
+  const int e0 = blockIdx.x * MDP_R;
+  const int nvalid = min(MDP_R, a.E - e0);
+  const int64_t next = a.ctl->next, len = a.ctl->len;
+  const uint32_t step = (uint32_t)a.ctl->env_steps;
+
+  for (int q = tid; q < MDP_R * 2 * ne; q += MDP_NT) {
+    const int r = q / (2 * ne), c = q - r * 2 * ne;
+    float pv = 0.f, vv = 0.f;
+    if (r < nvalid) {
+      pv = a.pos[(int64_t)(e0 + r) * 2 * ne + c];
+      vv = a.vel[(int64_t)(e0 + r) * 2 * ne + c];
+    }
+    sp[r * 2 * MDP_MAX_ENT + c] = pv;
+    sv[r * 2 * MDP_MAX_ENT + c] = vv;
+  }
+  for (int q = tid; q < MDP_R * ldr; q += MDP_NT) rowt[q] = 0.f;
+  __syncthreads();
+  int goal = 0;
+  if (tid < MDP_R) {
+    goal = tid < nvalid ? a.goal[e0 + tid] : 0;
+    for (int j = 0; j < n; ++j)
+      env_obs(E, sp + tid * 2 * MDP_MAX_ENT, sv + tid * 2 * MDP_MAX_ENT, goal, j, rowt + tid * ldr + T.ag[j].obs_off);
+  }
+  __syncthreads();
+
+  // policies: act_j = gumbel_softmax(actor_j(obs_j))  (MADDPGAgentTrainer.action)
+  for (int j = 0; j < n; ++j) {
+    const ADesc& aj = T.ag[j];
+    if (!a.act_in) mlp_fwd_tile<H>(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
+    if (tid < MDP_R) {
+      float* dst = rowt + tid * ldr + aj.act_off;
+      if (a.act_in) {
+        for (int k = 0; k < MDP_ACT_DIM; ++k)
+          dst[k] = tid < nvalid ? a.act_in[((int64_t)(e0 + tid) * n + j) * MDP_ACT_DIM + k] : 0.f;
+      } else {
+        float u[MDP_ACT_DIM];
+        if (a.u_in) {
+          for (int k = 0; k < MDP_ACT_DIM; ++k)
+            u[k] = tid < nvalid ? a.u_in[((int64_t)(e0 + tid) * n + j) * MDP_ACT_DIM + k] : 0.5f;
+        } else {
+          uniforms5(a.seed, 0x10000u | (uint32_t)j, step, (uint32_t)(a.env_base + e0 + tid), u);
+        }
+        gumbel_softmax5(lg + tid * 8, u, dst);
+      }
+    }
+    __syncthreads();
+  }
+
+  // physics, next obs, rewards, bookkeeping (one thread per env)
+  if (tid < nvalid) {
+    float* p = sp + tid * 2 * MDP_MAX_ENT;
+    float* v = sv + tid * 2 * MDP_MAX_ENT;
+    float* row = rowt + tid * ldr;
+    float actv[MDP_MAX_AGENTS * MDP_ACT_DIM];
+    for (int j = 0; j < n; ++j)
+      for (int k = 0; k < MDP_ACT_DIM; ++k) actv[j * MDP_ACT_DIM + k] = row[T.ag[j].act_off + k];
+    env_physics(E, p, v, actv);
+    float rew[MDP_MAX_AGENTS];
+    env_reward(E, p, goal, rew);
+    for (int j = 0; j < n; ++j) {
+      env_obs(E, p, v, goal, j, row + T.ag[j].nobs_off);
+      row[T.ag[j].rew_off] = rew[j];
+      row[T.ag[j].done_off] = 0.f;  // done_callback is None (environment.py _get_done)
+    }
+    const int e = e0 + tid;
+    float tot = 0.f;
+    for (int j = 0; j < n; ++j) {
+      const float r = a.ep_rew[(int64_t)e * n + j] + rew[j];
+      a.ep_rew[(int64_t)e * n + j] = r;
+      tot += r;
+    }
+    const int st = a.ep_step[e] + 1;
+    if (st >= E.max_ep_len) {  // terminal -> log episode, env.reset() (train.py:127-133)
+      const unsigned long long slot = atomicAdd((unsigned long long*)&a.ctl->episodes, 1ull);
+      float* lgp = a.eplog + (int64_t)(slot % (unsigned long long)a.eplog_cap) * (1 + n);
+      lgp[0] = tot;
+      for (int j = 0; j < n; ++j) {
+        lgp[1 + j] = a.ep_rew[(int64_t)e * n + j];
+        a.ep_rew[(int64_t)e * n + j] = 0.f;
+      }
+      int32_t g;
+      env_reset_one(E, a.seed, 0x20000u, step, (uint32_t)(a.env_base + e), p, v, &g);
+      a.goal[e] = g;
+      a.ep_step[e] = 0;
+    } else {
+      a.ep_step[e] = st;
+    }
+  }
+  __syncthreads();
+  // replay append of the 16 rows + env state store
+  const int v4 = T.row_stride >> 2;
+  for (int q = tid; q < nvalid * v4; q += MDP_NT) {
+    const int r = q / v4, c4 = q - r * v4;
+    const float* s = rowt + r * ldr + c4 * 4;
+    const int64_t dst = (next + e0 + r) % a.cap;
+    *reinterpret_cast<float4*>(a.replay + dst * T.row_stride + c4 * 4) = make_float4(s[0], s[1], s[2], s[3]);
+  }
+  for (int q = tid; q < nvalid * 2 * ne; q += MDP_NT) {
+    const int r = q / (2 * ne), c = q - r * 2 * ne;
+    a.pos[(int64_t)(e0 + r) * 2 * ne + c] = sp[r * 2 * MDP_MAX_ENT + c];
+    a.vel[(int64_t)(e0 + r) * 2 * ne + c] = sv[r * 2 * MDP_MAX_ENT + c];
+  }
+  if (last_block(a.ticket) && tid == 0) {
+    a.ctl->next = (next + a.E) % a.cap;
+    a.ctl->len = len + a.E < a.cap ? len + a.E : a.cap;
+    a.ctl->env_steps += 1;
+    *a.ticket = 0u;
+  }
+}
+
+// batched policy / critic evaluation for the facade (action, target_act, q_values)
+template <int H>
+__global__ __launch_bounds__(MDP_NT) void k_mlp_eval(EvalArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int ldx = lds_ld(a.in), ldh = H + 1;
+  LdsCarve cv(lds);
+  float* x = cv.take(MDP_R * ldx);
+  float* h1 = cv.take(MDP_R * ldh);
+  float* h2 = cv.take(MDP_R * ldh);
+  float* lg = cv.take(MDP_R * 8);
+  const int r0 = blockIdx.x * MDP_R;
+  const int nvalid = min(MDP_R, a.rows - r0);
+  for (int q = threadIdx.x; q < MDP_R * a.in; q += MDP_NT) {
+    const int r = q / a.in, c = q - r * a.in;
+    x[r * ldx + c] = r < nvalid ? a.x[(int64_t)(r0 + r) * a.in + c] : 0.f;
+  }
+  __syncthreads();
+  mlp_fwd_tile<H>(x, ldx, a.in, a.P, a.net, h1, h2, ldh, lg, 8);
+  const int tid = threadIdx.x;
+  if (tid < nvalid) {
+    const int row = r0 + tid;
+    if (a.gumbel) {
+      float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
+      if (a.u) {
+        for (int k = 0; k < MDP_ACT_DIM; ++k) u[k] = a.u[(int64_t)row * MDP_ACT_DIM + k];
+      } else {
+        uniforms5(a.seed, a.stream, a.ctr, (uint32_t)row, u);
+      }
+      gumbel_softmax5(lg + tid * 8, u, act);
+      for (int k = 0; k < MDP_ACT_DIM; ++k) a.out[(int64_t)row * MDP_ACT_DIM + k] = act[k];
+    } else {
+      for (int k = 0; k < a.net.out; ++k) a.out[(int64_t)row * a.net.out + k] = lg[tid * 8 + k];
+    }
+  }
+}
+
+// ================================================================ launchers
+#define MDP_CHECK_LAUNCH() \
+  do {                     \
+    hipError_t e_ = hipGetLastError(); \
+    if (e_ != hipSuccess) return e_;   \
+  } while (0)
+
+template <int H>
+static hipError_t launch_critic_grad_t(const CriticArgs& a, int lds_bytes, hipStream_t s) {
+  const int grid = (a.B + MDP_R - 1) / MDP_R;
+  hipLaunchKernelGGL(k_critic_grad<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+template <int H>
+static hipError_t launch_actor_grad_t(const ActorArgs& a, int lds_bytes, hipStream_t s) {
+  const int grid = (a.B + MDP_R - 1) / MDP_R;
+  hipLaunchKernelGGL(k_actor_grad<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+template <int H>
+static hipError_t launch_rollout_t(const RolloutArgs& a, int lds_bytes, hipStream_t s) {
+  const int grid = (a.E + MDP_R - 1) / MDP_R;
+  hipLaunchKernelGGL(k_rollout<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+template <int H>
+static hipError_t launch_eval_t(const EvalArgs& a, int lds_bytes, hipStream_t s) {
+  const int grid = (a.rows + MDP_R - 1) / MDP_R;
+  hipLaunchKernelGGL(k_mlp_eval<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+static int set_lds_limit_done = 0;
+template <int H>
+static void raise_lds_limits() {
+  (void)hipFuncSetAttribute((const void*)k_critic_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_actor_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_rollout<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_mlp_eval<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+static void ensure_lds_limits() {
+  if (!set_lds_limit_done) {
+    raise_lds_limits<64>();
+    raise_lds_limits<128>();
+    set_lds_limit_done = 1;
+  }
+}
+
+hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s) {
+  ensure_lds_limits();
+  return H == 64 ? launch_critic_grad_t<64>(a, lds_bytes, s) : launch_critic_grad_t<128>(a, lds_bytes, s);
+}
+hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s) {
+  ensure_lds_limits();
+  return H == 64 ? launch_actor_grad_t<64>(a, lds_bytes, s) : launch_actor_grad_t<128>(a, lds_bytes, s);
+}
+hipError_t mdp_launch_rollout(const RolloutArgs& a, int H, int lds_bytes, hipStream_t s) {
+  ensure_lds_limits();
+  return H == 64 ? launch_rollout_t<64>(a, lds_bytes, s) : launch_rollout_t<128>(a, lds_bytes, s);
+}
+hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t s) {
+  ensure_lds_limits();
+  return H == 64 ? launch_eval_t<64>(a, lds_bytes, s) : launch_eval_t<128>(a, lds_bytes, s);
+}
+hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s) {
+  const int grid = 6 + (a.polyak ? 6 : 0) + (a.stats_mode ? 1 : 0);
+  hipLaunchKernelGGL(k_apply, dim3(grid), dim3(256), 0, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+hipError_t mdp_launch_reduce(const ReduceArgs& a, hipStream_t s) {
+  const int grid = (int)((a.size + 255) / 256);
+  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_make_index, dim3(1), dim3(1024), 0, s, ctl, count, out);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
+                             hipStream_t s) {
+  const int64_t total = (int64_t)count * (stride >> 2);
+  int grid = (int)((total + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_gather_rows, dim3(grid), dim3(256), 0, s, replay, stride, idx, count, out);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+hipError_t mdp_launch_put_rows(float* replay, int stride, int64_t cap, int64_t next, const float* src, int64_t rows,
+                               hipStream_t s) {
+  const int64_t total = rows * (stride >> 2);
+  int grid = (int)((total + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_put_rows, dim3(grid), dim3(256), 0, s, replay, stride, cap, next, src, rows);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+hipError_t mdp_launch_put_agent(float* replay, int stride, const ADesc& ag, const int64_t* pos, const float* cols,
+                                int64_t rows, hipStream_t s) {
+  const int64_t total = rows * (2 * ag.obs_dim + MDP_ACT_DIM + 2);
+  int grid = (int)((total + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_put_agent, dim3(grid), dim3(256), 0, s, replay, stride, ag.obs_off, ag.act_off, ag.nobs_off,
+                     ag.rew_off, ag.done_off, ag.obs_dim, pos, cols, rows);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+hipError_t mdp_launch_env_reset(const EnvResetArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_env_reset, dim3((a.E + 255) / 256), dim3(256), 0, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+hipError_t mdp_launch_env_obs(const EnvObsArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_env_obs, dim3((a.E + 255) / 256), dim3(256), 0, s, a);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+// ring head / length written in stream order (facade adds and resets)
+__global__ void k_set_ring(Ctl* ctl, int64_t len, int64_t next) {
+  ctl->len = len;
+  ctl->next = next;
+}
+hipError_t mdp_launch_set_ring(Ctl* ctl, int64_t len, int64_t next, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_ring, dim3(1), dim3(1), 0, s, ctl, len, next);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}

@@ -1,0 +1,383 @@
+"""Engine: one libmaddpg_hip handle + its device arena (PyTorch storage only).
+
+Everything the reference keeps in the TF session (weights, targets, Adam
+slots, beta powers -- ``tf_util.py:189-214``) and in the per-agent Python
+replay lists (``replay_buffer.py``) lives in one device arena owned by a
+``torch.uint8`` CUDA tensor; all compute is launched by the HIP library on
+the engine's stream.  No CPU fallback exists: construction raises without a
+GPU or without the built library.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import MdpConfig, MdpTensorInfo
+
+TENSOR_NAMES = ("W1", "b1", "W2", "b2", "W3", "b3")
+
+
+class Engine:
+    def __init__(self, obs_dims, local_q=None, *, num_units=64, batch_size=1024, max_episode_len=25,
+                 capacity=int(1e6), num_envs=0, scenario="none", num_adversaries=0, lr=1e-2,
+                 gamma=0.95, tau=1e-2, grad_clip=0.5, actor_reg=1e-3, adam_b1=0.9, adam_b2=0.999,
+                 adam_eps=1e-8, seed=0, world_size=1, rank=0, device=None):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("maddpg_amd runs on a ROCm GPU only (no CPU fallback)")
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        n = len(obs_dims)
+        local_q = [False] * n if local_q is None else list(local_q)
+        self.n = n
+        self.obs_dims = [int(o) for o in obs_dims]
+        self.local_q = [bool(x) for x in local_q]
+        self.num_units = int(num_units)
+        self.batch_size = int(batch_size)
+        self.max_episode_len = int(max_episode_len)
+        self.capacity = int(capacity)
+        self.num_envs = int(num_envs)
+        self.scenario = scenario
+        self.world_size, self.rank = int(world_size), int(rank)
+        cfg = MdpConfig()
+        cfg.n_agents = n
+        for i in range(n):
+            cfg.obs_dim[i] = self.obs_dims[i]
+            cfg.local_q[i] = 1 if self.local_q[i] else 0
+        cfg.act_dim = _lib.ACT_DIM
+        cfg.num_units = self.num_units
+        cfg.batch_size = self.batch_size
+        cfg.max_episode_len = self.max_episode_len
+        cfg.capacity = self.capacity
+        cfg.num_envs = self.num_envs
+        cfg.scenario = _lib.SCN[scenario]
+        cfg.num_adversaries = int(num_adversaries)
+        cfg.world_size, cfg.rank = self.world_size, self.rank
+        cfg.lr, cfg.tau, cfg.grad_clip, cfg.actor_reg = lr, tau, grad_clip, actor_reg
+        cfg.adam_b1, cfg.adam_b2, cfg.adam_eps = adam_b1, adam_b2, adam_eps
+        cfg.gamma = float(gamma)
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.cfg = cfg
+        pt = ctypes.c_int64()
+        nbytes = self.lib.mdp_arena_bytes(ctypes.byref(cfg), ctypes.byref(pt))
+        if nbytes < 0:
+            raise ValueError("invalid maddpg configuration (see mdp_arena_bytes)")
+        self.param_floats = pt.value
+        with torch.cuda.device(self.device):
+            self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self.stream = torch.cuda.Stream(device=self.device)
+            h = ctypes.c_void_p()
+            rc = self.lib.mdp_create(ctypes.byref(cfg), ctypes.c_void_p(self.arena.data_ptr()), nbytes,
+                                     ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(h))
+        self.h = h
+        if rc != 0:
+            msg = self.lib.mdp_last_error(h).decode()
+            self.lib.mdp_destroy(h)
+            self.h = None
+            raise ValueError(f"mdp_create failed: {msg}")
+        lay = (ctypes.c_int32 * 6)()
+        self.row_layout = []
+        for i in range(n):
+            self._c("mdp_row_layout", i, lay)
+            self.row_layout.append(tuple(lay[:6]))
+        self.row_stride = self.row_layout[0][5]
+        self._tensors = {}
+        for i in range(n):
+            for net in (0, 1):
+                infos = []
+                for t in range(6):
+                    ti = MdpTensorInfo()
+                    self._c("mdp_tensor", i, net, t, ctypes.byref(ti))
+                    infos.append((ti.offset, ti.rows, ti.cols))
+                self._tensors[(i, net)] = infos
+
+    # ------------------------------------------------------------ plumbing
+    def _c(self, name, *args):
+        rc = getattr(self.lib, name)(self.h, *args)
+        return _lib.check(self.lib, self.h, rc, name)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mdp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync_in(self):
+        """engine stream waits for work torch queued on the current stream"""
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+
+    def sync_out(self):
+        """torch's current stream waits for the engine stream"""
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def synchronize(self):
+        self._c("mdp_synchronize")
+
+    @staticmethod
+    def _ptr(t):
+        return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+    def region(self, name, dtype=torch.float32):
+        off, nb = ctypes.c_int64(), ctypes.c_int64()
+        self._c("mdp_region", _lib.REGION[name], ctypes.byref(off), ctypes.byref(nb))
+        isz = torch.tensor([], dtype=dtype).element_size()
+        return self.arena[off.value: off.value + (nb.value // isz) * isz].view(dtype)
+
+    def net_tensors(self, agent, net):
+        return self._tensors[(agent, net)]
+
+    def grad_view(self, agent, net):
+        """float32 view of one net's gradient in the GRAD region (all-reduce target)."""
+        infos = self._tensors[(agent, net)]
+        start = infos[0][0]
+        end = infos[5][0] + ((infos[5][1] * infos[5][2] + 3) // 4) * 4
+        return self.region("grad")[start:end]
+
+    # ---------------------------------------------------------- parameters
+    def _flat_shapes(self, agent, which):
+        net = 1 if "critic" in which else 0
+        return [(r, c) for (_o, r, c) in self._tensors[(agent, net)]]
+
+    def set_params(self, agent, which, params):
+        shapes = self._flat_shapes(agent, which)
+        if isinstance(params, dict):
+            parts = [np.asarray(params[k], np.float32).reshape(s) for k, s in zip(TENSOR_NAMES, shapes)]
+            flat = np.concatenate([p.ravel() for p in parts])
+        else:
+            flat = np.asarray(params, np.float32).ravel()
+        flat = np.ascontiguousarray(flat, np.float32)
+        self._c("mdp_set_params", agent, _lib.WHICH[which], _lib.fptr(flat), flat.size)
+
+    def get_params(self, agent, which):
+        shapes = self._flat_shapes(agent, which)
+        n = sum(r * c for r, c in shapes)
+        flat = np.empty(n, np.float32)
+        self._c("mdp_get_params", agent, _lib.WHICH[which], _lib.fptr(flat), n)
+        out, s = {}, 0
+        for k, (r, c) in zip(TENSOR_NAMES, shapes):
+            a = flat[s:s + r * c].reshape(r, c)
+            out[k] = a[0].copy() if k.startswith("b") else a.copy()
+            s += r * c
+        return out
+
+    def get_beta_powers(self, agent, net):
+        b = np.empty(2, np.float32)
+        self._c("mdp_get_beta_powers", agent, net, _lib.fptr(b))
+        return b
+
+    def set_beta_powers(self, agent, net, b):
+        b = np.ascontiguousarray(b, np.float32)
+        self._c("mdp_set_beta_powers", agent, net, _lib.fptr(b))
+
+    def init_params(self, seed=0):
+        """tf.contrib.layers xavier_initializer (uniform) for all four nets per
+        agent, each drawn independently (targets are NOT copies: maddpg.py:66,104)."""
+        rng = np.random.default_rng(seed)
+        H = self.num_units
+        for i in range(self.n):
+            for which in ("actor", "critic", "tgt_actor", "tgt_critic"):
+                shapes = self._flat_shapes(i, which)
+                p = {}
+                for k, (r, c) in zip(TENSOR_NAMES, shapes):
+                    if k.startswith("W"):
+                        lim = np.sqrt(6.0 / (r + c))
+                        p[k] = rng.uniform(-lim, lim, size=(r, c)).astype(np.float32)
+                    else:
+                        p[k] = np.zeros((r, c), np.float32)
+                self.set_params(i, which, p)
+        return H
+
+    # ------------------------------------------------------------- replay
+    def buffer_len(self):
+        return int(self.lib.mdp_buffer_len(self.h))
+
+    def add_rows(self, rows):
+        rows = rows.to(self.device, torch.float32).contiguous()
+        assert rows.dim() == 2 and rows.shape[1] == self.row_stride
+        self.sync_in()
+        self._c("mdp_buffer_add_rows", self._ptr(rows), rows.shape[0])
+        self._keep = rows  # keep alive until the stream consumed it
+        self.sync_out()
+
+    def put_agent(self, agent, pos, cols):
+        pos = pos.to(self.device, torch.int64).contiguous()
+        cols = cols.to(self.device, torch.float32).contiguous()
+        self.sync_in()
+        self._c("mdp_buffer_put_agent", agent, self._ptr(pos), self._ptr(cols), pos.shape[0])
+        self.sync_out()
+
+    def set_ring(self, length, next_idx):
+        self._c("mdp_buffer_set_len", int(length), int(next_idx))
+
+    def seed_py_random(self, seed):
+        self._c("mdp_seed_py_random", int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+    def set_rng_state(self, state625):
+        st = np.ascontiguousarray(np.asarray(state625, dtype=np.uint64).astype(np.uint32))
+        assert st.size == 625
+        self._c("mdp_set_rng_state", st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+
+    def get_rng_state(self):
+        st = np.empty(625, np.uint32)
+        self._c("mdp_get_rng_state", st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        return st
+
+    def make_index(self, count, out=None):
+        if out is None:
+            out = torch.empty(count, dtype=torch.int32, device=self.device)
+        self.sync_in()
+        self._c("mdp_make_index", int(count), self._ptr(out))
+        self.sync_out()
+        return out
+
+    def sample_rows(self, idx, out=None):
+        idx = idx.to(self.device, torch.int32).contiguous()
+        if out is None:
+            out = torch.empty((idx.shape[0], self.row_stride), dtype=torch.float32, device=self.device)
+        self.sync_in()
+        self._c("mdp_sample_rows", self._ptr(idx), idx.shape[0], self._ptr(out))
+        self.sync_out()
+        return out
+
+    # ------------------------------------------------------------ policies
+    def act(self, agent, obs, target=False, u=None):
+        obs = obs.to(self.device, torch.float32).contiguous()
+        out = torch.empty((obs.shape[0], _lib.ACT_DIM), dtype=torch.float32, device=self.device)
+        if u is not None:
+            u = u.to(self.device, torch.float32).contiguous()
+        self.sync_in()
+        self._c("mdp_act", agent, 1 if target else 0, self._ptr(obs), self._ptr(out), obs.shape[0], self._ptr(u))
+        self.sync_out()
+        return out
+
+    def actor_logits(self, agent, obs, target=False):
+        obs = obs.to(self.device, torch.float32).contiguous()
+        out = torch.empty((obs.shape[0], _lib.ACT_DIM), dtype=torch.float32, device=self.device)
+        self.sync_in()
+        self._c("mdp_actor_logits", agent, 1 if target else 0, self._ptr(obs), self._ptr(out), obs.shape[0])
+        self.sync_out()
+        return out
+
+    def q_values(self, agent, x, target=False):
+        x = x.to(self.device, torch.float32).contiguous()
+        out = torch.empty(x.shape[0], dtype=torch.float32, device=self.device)
+        self.sync_in()
+        self._c("mdp_q_values", agent, 1 if target else 0, self._ptr(x), self._ptr(out), x.shape[0])
+        self.sync_out()
+        return out
+
+    # ------------------------------------------------------------ training
+    def update(self, agent, idx=None, u_tgt=None, u_act=None):
+        args = []
+        for t, dt in ((idx, torch.int32), (u_tgt, torch.float32), (u_act, torch.float32)):
+            args.append(None if t is None else t.to(self.device, dt).contiguous())
+        self.sync_in()
+        self._c("mdp_update", agent, *[self._ptr(a) for a in args])
+        self._keep = args
+        self.sync_out()
+
+    def update_gate(self, t):
+        return self._c("mdp_update_gate", int(t))
+
+    def update_round(self):
+        self._c("mdp_update_round")
+
+    def critic_grad(self, agent, idx, u_tgt=None):
+        self._c("mdp_critic_grad", agent, self._ptr(idx), self._ptr(u_tgt))
+
+    def actor_grad(self, agent, idx, u_act=None):
+        self._c("mdp_actor_grad", agent, self._ptr(idx), self._ptr(u_act))
+
+    def reduce_grad(self, agent, net):
+        self._c("mdp_reduce_grad", agent, net)
+
+    def apply_grad(self, agent, net, scale=1.0):
+        self._c("mdp_apply_grad", agent, net, float(scale))
+
+    def index_slot(self, agent):
+        """int32 view of the device index slot used by agent's update this round."""
+        return self.region("index", torch.int32)[agent * self.batch_size:(agent + 1) * self.batch_size]
+
+    def stats(self, agent):
+        out = (ctypes.c_double * 6)()
+        self._c("mdp_get_stats", agent, out)
+        return list(out)
+
+    # ----------------------------------------------------------------- env
+    @property
+    def n_entities(self):
+        """agents + landmarks (scenario make_world)."""
+        landmarks = {"simple": 1, "simple_spread": self.n, "simple_adversary": self.n - 1,
+                     "simple_tag": 2}.get(self.scenario, 0)
+        return self.n + landmarks
+
+    def env_reset(self):
+        self._c("mdp_env_reset")
+
+    def env_step(self, act_in=None, u=None):
+        a = None if act_in is None else act_in.to(self.device, torch.float32).contiguous()
+        uu = None if u is None else u.to(self.device, torch.float32).contiguous()
+        if a is not None or uu is not None:
+            self.sync_in()
+        self._c("mdp_env_step", self._ptr(a), self._ptr(uu))
+        if a is not None or uu is not None:
+            self._keep = (a, uu)
+            self.sync_out()
+
+    def env_state(self):
+        E, ne = self.num_envs, self.n_entities
+        pos = np.empty((E, ne, 2), np.float32)
+        vel = np.empty((E, ne, 2), np.float32)
+        goal = np.empty(E, np.int32)
+        step = np.empty(E, np.int32)
+        self._c("mdp_env_get_state", _lib.fptr(pos), _lib.fptr(vel),
+                goal.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                step.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        return {"pos": pos, "vel": vel, "goal": goal, "ep_step": step}
+
+    def set_env_state(self, pos, vel, goal=None, ep_step=None):
+        E = self.num_envs
+        pos = np.ascontiguousarray(pos, np.float32)
+        vel = np.ascontiguousarray(vel, np.float32)
+        goal = np.ascontiguousarray(np.zeros(E) if goal is None else goal, np.int32)
+        ep_step = np.ascontiguousarray(np.zeros(E) if ep_step is None else ep_step, np.int32)
+        self._c("mdp_env_set_state", _lib.fptr(pos), _lib.fptr(vel),
+                goal.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                ep_step.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+
+    def env_obs(self):
+        out = torch.empty((self.num_envs, sum(self.obs_dims)), dtype=torch.float32, device=self.device)
+        self._c("mdp_env_obs", self._ptr(out))
+        self.sync_out()
+        return out
+
+    def episode_count(self):
+        n = self.lib.mdp_episode_count(self.h)
+        if n < 0:
+            raise _lib.MdpError("mdp_episode_count failed")
+        return int(n)
+
+    def episode_log(self, first, n):
+        out = np.empty((n, 1 + self.n), np.float32)
+        if n:
+            self._c("mdp_episode_log", int(first), int(n), _lib.fptr(out))
+        return out
+
+    def replay_rows(self, start, count):
+        """float32 view [count, row_stride] of the replay region (no copy)."""
+        r = self.region("replay")
+        return r[start * self.row_stride:(start + count) * self.row_stride].view(count, self.row_stride)
+
+    # ---------------------------------------------------------- profiling
+    def prof_enable(self, kind, on=True):
+        self._c("mdp_prof_enable", _lib.KERNEL[kind], 1 if on else 0)
+
+    def prof_read(self, kind):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        self._c("mdp_prof_read", _lib.KERNEL[kind], ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value

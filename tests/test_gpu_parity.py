@@ -1,0 +1,305 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+fixtures and the CPU oracle, on identical seeded inputs.
+
+Tolerances (north_star): replay index selection and gathers bit-exact; critic
+loss within 1e-5 (relative, fp32); parameters after a full update within the
+fp32 accumulation-order noise stated per test.
+"""
+import copy
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from maddpg_amd.engine import Engine  # noqa: E402
+from oracle import mpe, nets, trainer  # noqa: E402
+from tests.helpers import (case_names, golden_case, joint_rows, row_layout,  # noqa: E402
+                           synthetic_trainer_case)
+
+ACT = 5
+
+
+def _digest(arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def _engine_with_case(c, **kw):
+    eng = Engine(c["dims"], batch_size=c["B"], capacity=c["cap"], **kw)
+    rows = joint_rows(c["data"](), c["dims"])
+    eng.add_rows(torch.from_numpy(rows))
+    assert eng.buffer_len() == min(c["cap"], c["n_added"])
+    return eng
+
+
+# ------------------------------------------------------------- replay index
+@pytest.mark.parametrize("name", ["spread_s0", "spread_s1", "spread_s12345", "simple_s0", "wrap_s1",
+                                  "tag6_s0", "tag6_s12345", "small_s1"])
+def test_make_index_bit_exact_vs_reference(golden, name):
+    c = golden_case(golden, name)
+    eng = _engine_with_case(c)
+    eng.seed_py_random(c["seed"])
+    n, B = len(c["dims"]), c["B"]
+    idx = eng.make_index(n * B).cpu().numpy().reshape(n, B)
+    np.testing.assert_array_equal(idx, c["idx"])
+    np.testing.assert_array_equal(eng.get_rng_state(), c["state"])
+    # per-agent draws (maddpg.py:167 called agent by agent) give the same stream
+    eng.seed_py_random(c["seed"])
+    for i in range(n):
+        np.testing.assert_array_equal(eng.make_index(B).cpu().numpy(), c["idx"][i])
+    np.testing.assert_array_equal(eng.get_rng_state(), c["state"])
+
+
+@pytest.mark.parametrize("name", ["spread_s0", "wrap_s12345", "tag6_s1", "small_s0", "simple_s12345"])
+def test_fused_gather_bit_exact_vs_reference(golden, name):
+    c = golden_case(golden, name)
+    eng = _engine_with_case(c)
+    lay, stride = row_layout(c["dims"])
+    n = len(c["dims"])
+    for i in range(n):
+        rows = eng.sample_rows(torch.from_numpy(c["idx"][i])).cpu().numpy()
+        arrs = []
+        for j in range(n):
+            lj, o = lay[j], c["dims"][j]
+            arrs += [rows[:, lj["obs"]:lj["obs"] + o].astype(np.float64),
+                     rows[:, lj["act"]:lj["act"] + ACT].astype(np.float32),
+                     rows[:, lj["nobs"]:lj["nobs"] + o].astype(np.float64)]
+        arrs += [rows[:, lay[i]["rew"]].astype(np.float64), rows[:, lay[i]["done"]].astype(np.float64)]
+        assert _digest(arrs) == c["sha"][i], f"agent {i}"
+
+
+def test_make_index_continues_python_global_state():
+    random.seed(99)
+    for _ in range(37):
+        random.random()
+    eng = Engine([4], batch_size=8, capacity=5000)
+    eng.add_rows(torch.zeros((3333, eng.row_stride)))
+    eng.set_rng_state(np.array(random.getstate()[1], dtype=np.uint64))
+    got = eng.make_index(2000).cpu().numpy()
+    want = [random.randint(0, 3332) for _ in range(2000)]
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(eng.get_rng_state(), np.array(random.getstate()[1], np.uint32))
+
+
+def test_make_index_edge_lengths():
+    eng = Engine([4], batch_size=8, capacity=70000)
+    for L in (1, 2, 3, 624, 625, 65536, 65537):
+        eng.set_ring(L, L % 70000)
+        g = random.Random(L)
+        eng.set_rng_state(np.array(g.getstate()[1], dtype=np.uint64))
+        got = eng.make_index(1500).cpu().numpy()
+        np.testing.assert_array_equal(got, [g.randint(0, L - 1) for _ in range(1500)])
+
+
+# ----------------------------------------------------------- policy / critic
+def test_act_and_q_values_match_oracle():
+    dims = [18, 18, 18]
+    c = synthetic_trainer_case(dims, B=100, L=100, seed=11)
+    eng = Engine(dims, batch_size=100, capacity=200)
+    for i, p in enumerate(c["params"]):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            eng.set_params(i, w, p[w])
+    obs = c["data"][1][0][:100].astype(np.float32)
+    u = c["u_act"][1][:100]
+    got = eng.act(1, torch.from_numpy(obs), u=torch.from_numpy(u)).cpu().numpy()
+    ag = trainer.AgentParams(**c["params"][1])
+    np.testing.assert_allclose(got, trainer.act(ag, obs, u), atol=2e-6)
+    got_t = eng.act(1, torch.from_numpy(obs), target=True, u=torch.from_numpy(u)).cpu().numpy()
+    np.testing.assert_allclose(got_t, trainer.target_act(ag, obs, u), atol=2e-6)
+    lg = eng.actor_logits(1, torch.from_numpy(obs)).cpu().numpy()
+    np.testing.assert_allclose(lg, nets.mlp_fwd(ag.actor, obs)[0], atol=2e-5)
+    x = np.random.default_rng(0).normal(size=(77, 69)).astype(np.float32)
+    q = eng.q_values(1, torch.from_numpy(x), target=True).cpu().numpy()
+    np.testing.assert_allclose(q, nets.mlp_fwd(ag.tgt_critic, x)[0][:, 0], rtol=1e-5, atol=2e-5)
+
+
+# ------------------------------------------------------------------ update
+def _update_parity(dims, B, L, seed, local_q=None, H=64, check_round=True):
+    c = synthetic_trainer_case(dims, B, L, seed, local_q, H)
+    n = len(dims)
+    eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L + 7)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    for i, p in enumerate(c["params"]):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            eng.set_params(i, w, p[w])
+    agents = [trainer.AgentParams(**copy.deepcopy(p), local_q=c["local_q"][i]) for i, p in enumerate(c["params"])]
+    report = []
+    for i in range(n if check_round else 1):
+        eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
+                   u_act=torch.from_numpy(c["u_act"][i]))
+        got = eng.stats(i)
+        want, _ = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i])
+        # critic loss (pre-update) within 1e-5 relative; other stats fp64 reductions of fp32 values
+        assert abs(got[0] - want[0]) <= 1e-5 * abs(want[0]) + 1e-7, (got[0], want[0])
+        np.testing.assert_allclose(got[1:], want[1:], rtol=2e-5, atol=2e-6)
+        for w, ref in (("actor", agents[i].actor), ("critic", agents[i].critic),
+                       ("tgt_actor", agents[i].tgt_actor), ("tgt_critic", agents[i].tgt_critic)):
+            dev = eng.get_params(i, w)
+            for k in ref:
+                err = np.abs(dev[k] - ref[k].reshape(dev[k].shape))
+                report.append((i, w, k, float(err.max())))
+                # one Adam step moves each weight by <= ~lr; differences come from
+                # fp32 reduction order only (sign-unstable near-zero gradients excepted)
+                assert err.max() < 2e-4, (i, w, k, float(err.max()))
+        for net in (0, 1):
+            bp = eng.get_beta_powers(i, net)
+            opt = agents[i].opt_actor if net == 0 else agents[i].opt_critic
+            assert bp[0] == opt.b1p and bp[1] == opt.b2p
+    worst = max(r[3] for r in report)
+    print(f"update parity dims={dims} B={B} H={H} local_q={c['local_q']}: worst param |diff| = {worst:.3e}")
+    return worst
+
+
+def test_update_parity_spread_b1024():
+    _update_parity([18, 18, 18], B=1024, L=4000, seed=21)
+
+
+def test_update_parity_simple():
+    _update_parity([4], B=1024, L=2000, seed=22)
+
+
+def test_update_parity_adversary_mixed_ddpg():
+    _update_parity([8, 10, 10], B=512, L=3000, seed=23, local_q=[True, False, False])
+
+
+def test_update_parity_ragged_batch():
+    _update_parity([18, 18, 18], B=200, L=900, seed=24)
+
+
+def test_update_parity_tag6_h128():
+    _update_parity([22, 22, 22, 22, 20, 20], B=256, L=1500, seed=25, H=128)
+
+
+def test_update_round_uses_device_index_stream():
+    """mdp_update_round draws agent 0's B indices first, then agent 1's ...
+    (maddpg.py:167 per agent, train.py:160-161 agent order) from the MT stream."""
+    dims = [18, 18, 18]
+    B, L = 256, 3000
+    c = synthetic_trainer_case(dims, B, L, seed=31)
+    eng = Engine(dims, batch_size=B, capacity=L)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    eng.init_params(5)
+    eng.seed_py_random(1234)
+    eng.update_round()
+    eng.synchronize()
+    g = random.Random(1234)
+    want = np.array([[g.randint(0, L - 1) for _ in range(B)] for _ in range(3)])
+    got = eng.region("index", torch.int32)[:3 * B].cpu().numpy().reshape(3, B)
+    np.testing.assert_array_equal(got, want)
+    for i in range(3):
+        assert all(np.isfinite(eng.stats(i)))
+
+
+# --------------------------------------------------------------------- env
+SCENARIOS = [("simple", 1, 0), ("simple_spread", 3, 0), ("simple_adversary", 3, 1),
+             ("simple_tag", 4, 3), ("simple_tag", 6, 4)]
+
+
+def _oracle_scn(name, n, na):
+    if name == "simple_tag":
+        return mpe.SimpleTag(n_adv=na, n_good=n - na)
+    if name == "simple_adversary":
+        return mpe.SimpleAdversary(n_good=n - na, n_adv=na)
+    if name == "simple_spread":
+        return mpe.SimpleSpread(n)
+    return mpe.Simple()
+
+
+@pytest.mark.parametrize("name,n,na", SCENARIOS)
+def test_env_step_parity(name, n, na):
+    from maddpg_amd.envs import spec
+    sp = spec(name, n, na if na else None)
+    E = 37   # ragged: not a multiple of the 16-env tile
+    eng = Engine(sp.obs_dims, batch_size=16, capacity=1000, num_envs=E, scenario=name,
+                 num_adversaries=sp.num_adversaries, max_episode_len=25, seed=3)
+    eng.env_reset()
+    st = eng.env_state()
+    assert np.all(np.abs(st["pos"]) <= 1.0) and np.all(st["vel"] == 0)
+    sc = _oracle_scn(name, n, na)
+    rng = np.random.default_rng(4)
+    # move away from the reset state so velocities are non-zero
+    for step in range(3):
+        z = rng.normal(size=(E, n, ACT))
+        act = (np.exp(z) / np.exp(z).sum(-1, keepdims=True)).astype(np.float32)
+        st = eng.env_state()
+        ost = {"pos": st["pos"].astype(np.float64), "vel": st["vel"].astype(np.float64), "goal": st["goal"]}
+        obs0 = sc.observation(ost)
+        nst, obs1, rew = sc.step(ost, act.astype(np.float64))
+        eng.env_step(act_in=torch.from_numpy(act))
+        got = eng.env_state()
+        np.testing.assert_allclose(got["pos"], nst["pos"], atol=2e-5)
+        np.testing.assert_allclose(got["vel"], nst["vel"], atol=2e-5)
+        rows = eng.replay_rows(step * E, E).cpu().numpy()
+        lay, _ = row_layout(sp.obs_dims)
+        for j in range(n):
+            lj, o = lay[j], sp.obs_dims[j]
+            np.testing.assert_allclose(rows[:, lj["obs"]:lj["obs"] + o], obs0[j], atol=2e-5)
+            np.testing.assert_array_equal(rows[:, lj["act"]:lj["act"] + ACT], act[:, j])
+            np.testing.assert_allclose(rows[:, lj["nobs"]:lj["nobs"] + o], obs1[j], atol=2e-5)
+            np.testing.assert_allclose(rows[:, lj["rew"]], rew[:, j], rtol=1e-5, atol=5e-5)
+            assert np.all(rows[:, lj["done"]] == 0)
+    assert eng.buffer_len() == 3 * E
+
+
+def test_env_episode_reset_and_log():
+    from maddpg_amd.envs import spec
+    sp = spec("simple_spread")
+    E = 20
+    eng = Engine(sp.obs_dims, batch_size=16, capacity=1000, num_envs=E, scenario="simple_spread",
+                 max_episode_len=3, seed=8)
+    eng.env_reset()
+    eng.init_params(0)
+    for _ in range(3):
+        eng.env_step()
+    st = eng.env_state()
+    assert np.all(st["ep_step"] == 0)
+    assert eng.episode_count() == E
+    log = eng.episode_log(0, E)
+    rows = eng.replay_rows(0, 3 * E).cpu().numpy()
+    lay, _ = row_layout(sp.obs_dims)
+    per_env = sum(rows[k * E:(k + 1) * E, lay[j]["rew"]] for k in range(3) for j in range(3))
+    np.testing.assert_allclose(np.sort(log[:, 0]), np.sort(per_env), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(log[:, 0], log[:, 1:].sum(1), rtol=1e-5, atol=1e-4)
+
+
+def test_rollout_policy_actions_match_oracle():
+    from maddpg_amd.envs import spec
+    sp = spec("simple_spread")
+    E = 40
+    eng = Engine(sp.obs_dims, batch_size=16, capacity=1000, num_envs=E, scenario="simple_spread", seed=9)
+    eng.init_params(3)
+    eng.env_reset()
+    obs = eng.env_obs().cpu().numpy()
+    u = np.random.default_rng(2).uniform(1e-6, 1, size=(E, 3, ACT)).astype(np.float32)
+    eng.env_step(u=torch.from_numpy(u))
+    rows = eng.replay_rows(0, E).cpu().numpy()
+    lay, _ = row_layout(sp.obs_dims)
+    for j in range(3):
+        p = eng.get_params(j, "actor")
+        logits = nets.mlp_fwd(p, obs[:, lay[j]["obs"]:lay[j]["obs"] + 18])[0]
+        want = nets.gumbel_softmax(logits, u[:, j])
+        np.testing.assert_allclose(rows[:, lay[j]["act"]:lay[j]["act"] + ACT], want, atol=2e-6)
+
+
+# ---------------------------------------------------- size-independent checks
+def test_full_size_index_stream_properties():
+    """BASELINE S3-sized draw (1e6-row ring, 6 x 4096 indices): bit-exact vs
+    CPython and the stream position continues correctly across calls."""
+    eng = Engine([18, 18, 18], batch_size=4096, capacity=1_000_000)
+    eng.set_ring(1_000_000, 0)
+    eng.seed_py_random(2024)
+    g = random.Random(2024)
+    for _ in range(3):
+        got = eng.make_index(6 * 4096).cpu().numpy()
+        want = [g.randint(0, 999_999) for _ in range(6 * 4096)]
+        np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(eng.get_rng_state(), np.array(g.getstate()[1], np.uint32))
