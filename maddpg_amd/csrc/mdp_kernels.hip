@@ -1114,15 +1114,16 @@ static hipError_t launch_eval_t(const EvalArgs& a, int lds_bytes, hipStream_t s)
 static int set_lds_limit_done = 0;
 template <int H>
 static void raise_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_critic_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)k_actor_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)k_rollout<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)k_mlp_eval<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_critic_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_actor_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_rollout<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_mlp_eval<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
 }
 static void ensure_lds_limits() {
   if (!set_lds_limit_done) {
     raise_lds_limits<64>();
     raise_lds_limits<128>();
+    (void)hipGetLastError();  // an unsupported opt-in must not poison the next launch check
     set_lds_limit_done = 1;
   }
 }
