@@ -1,0 +1,217 @@
+"""Benchmark: MADDPG training loop on MI355X (BASELINE.json metric).
+
+metric: env-steps/sec (+ trainer-updates/sec), simple_spread N=3, batch 1024.
+A "step" is one vector env step of E env copies per rank (actors + Gumbel +
+MPE physics + replay append, all on the device) plus the update rounds the
+reference cadence makes due (one round = every agent's update, per 100
+transitions per rank, maddpg.py:164).  The replay is prefilled to the
+reference's gate (batch*max_episode_len rows) before warm-up, so every timed
+step trains.  `value` = env transitions of all ranks / wall time (max over
+ranks) with everything resident in HBM.
+
+    python bench.py                        # N=1, E=1024 (BASELINE configs[1])
+    torchrun --nproc-per-node N bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from maddpg_amd import _lib  # noqa: E402
+from maddpg_amd.parallel import init_process_group_from_env  # noqa: E402
+from maddpg_amd.runner import VecRunner  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix/vector dense peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+
+
+def flops_critic_grad(eng, agent):
+    """algorithmic flops of one k_critic_grad launch (batch B, agent's critic step)."""
+    H, B = eng.num_units, eng.batch_size
+    dims = eng.obs_dims
+    lq = eng.local_q[agent]
+    cin = dims[agent] + 5 if lq else sum(dims) + 5 * eng.n
+    actors = [agent] if lq else range(eng.n)
+    mac = sum(dims[j] * H + H * H + 5 * H for j in actors)       # target actors
+    mac += 2 * (cin * H + H * H + H)                              # target critic + critic fwd
+    mac += 2 * H * H + cin * H + 2 * H                            # critic backward (dW3,dh2,dW2,dh1,dW1)
+    return 2.0 * B * mac
+
+
+def flops_actor_grad(eng, agent):
+    H, B = eng.num_units, eng.batch_size
+    o = eng.obs_dims[agent]
+    cin = o + 5 if eng.local_q[agent] else sum(eng.obs_dims) + 5 * eng.n
+    mac = 2 * o * H + 5 * H * H + cin * H + 22 * H
+    return 2.0 * B * mac
+
+
+def bytes_rollout(eng):
+    ne = eng.n_entities
+    per_env = 4 * eng.row_stride + 2 * 2 * (4 * 2 * ne) + 16 + 4 * eng.n
+    return per_env * eng.num_envs
+
+
+def roofline_for(kind, eng, ms_avg):
+    if kind in ("critic_grad", "actor_grad"):
+        f = flops_critic_grad if kind == "critic_grad" else flops_actor_grad
+        fl = sum(f(eng, i) for i in range(eng.n)) / eng.n
+        ach = fl / (ms_avg * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 4), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 6), "traffic": None,
+                "kernel": f"k_{kind}", "algorithmic_per_launch": fl, "avg_launch_ms": ms_avg}
+    if kind == "rollout":
+        by = bytes_rollout(eng)
+    else:
+        return None
+    ach = by / (ms_avg * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None, "kernel": f"k_{kind}",
+            "algorithmic_per_launch": by, "avg_launch_ms": ms_avg}
+
+
+def load_traffic(kernel, config_key):
+    """per-launch HBM bytes from a committed rocprofv3 PMC summary (profiles/pmc_*.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        ent = d.get(config_key, {}).get(kernel)
+        return None if ent is None else ent.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(args):
+    env = dict(os.environ)
+    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        env[k] = "1"
+    cmd = [sys.executable, "-m", "oracle.train_loop", "--scenario", args.scenario,
+           "--seconds", str(args.cpu_seconds), "--batch-size", str(args.batch_size),
+           "--num-units", str(args.num_units), "--pin-core", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.cpu_seconds * 6 + 120)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": round(out["env_steps_per_sec"], 3), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "trainer_updates_per_sec": round(out["trainer_updates_per_sec"], 3),
+            "sample": (f"oracle/train_loop.py: {args.scenario} N=3, 1 env, batch {args.batch_size}, "
+                       f"{args.num_units}-unit MLPs, reference call structure (batch-1 action per agent, "
+                       f"Python-list replay, sequential per-agent updates every 100 steps), numpy fp32 on "
+                       f"1 pinned core, replay prefilled to the gate; {out['env_steps']} env steps + "
+                       f"{out['updates']} updates in {out['seconds']:.1f} s")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scenario", default="simple_spread")
+    ap.add_argument("--num-envs", type=int, default=1024)
+    ap.add_argument("--batch-size", type=int, default=1024)
+    ap.add_argument("--num-units", type=int, default=64)
+    ap.add_argument("--train-every", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rollout-only", action="store_true", help="time env steps without training")
+    args = ap.parse_args()
+
+    world, rank, local = init_process_group_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    r = VecRunner(args.scenario, args.num_envs, batch_size=args.batch_size, num_units=args.num_units,
+                  seed=args.seed, train_every=args.train_every, world_size=world, rank=rank)
+    eng = r.eng
+    r.prefill()
+    kinds = [k for k in _lib.KERNEL]
+    for k in kinds:
+        eng.prof_enable(k, True)
+
+    def one_step():
+        if args.rollout_only:
+            r.rollout()
+            return 0
+        return r.step()
+
+    for _ in range(args.warmup):
+        one_step()
+    r.synchronize()
+    per_kind = {k: eng.prof_read(k) for k in kinds}
+    for k in kinds:
+        eng.prof_enable(k, False)
+    dominant = max(per_kind, key=lambda k: per_kind[k][0])
+    eng.prof_enable(dominant, True)   # live HIP events on the engine stream, timed region only
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rounds = 0
+    for _ in range(args.steps):
+        rounds += one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_tot, launches = eng.prof_read(dominant)
+    eng.prof_enable(dominant, False)
+
+    env_steps = args.num_envs * args.steps * world
+    updates = rounds * r.n           # optimiser updates (each on world*B samples)
+    value = env_steps / dt
+    roof = roofline_for(dominant, eng, ms_tot / max(launches, 1)) if launches else None
+    cfg_key = f"{args.scenario}_E{args.num_envs}_B{args.batch_size}_H{args.num_units}"
+    if roof is not None:
+        tr = load_traffic(roof["kernel"], cfg_key)
+        roof["traffic"] = tr
+    if rank == 0:
+        out = {
+            "metric": "env-steps/sec (end-to-end at the reference update cadence), simple_spread N=3, batch 1024",
+            "value": round(value, 3),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (random-init weights, device MPE env rollouts)",
+            "config": {"workload": f"{args.scenario} N={r.n}, {args.num_envs} env copies per GPU, batch "
+                                   f"{args.batch_size}, {args.num_units}-unit MLPs, 1 update round per "
+                                   f"{args.train_every} transitions per rank",
+                       "scenario": args.scenario, "num_envs_per_gpu": args.num_envs,
+                       "global_batch": args.batch_size * world, "parallelism": f"dp{world}",
+                       "mode": "rollout-only" if args.rollout_only else "strict"},
+            "trainer_updates_per_sec": round(updates / dt, 3),
+            "update_rounds": rounds,
+            "per_kernel_warmup_ms": {k: round(v[0], 4) for k, v in per_kind.items()},
+            "roofline": roof,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

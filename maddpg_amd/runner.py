@@ -1,0 +1,102 @@
+"""Vectorised, device-resident version of ``experiments/train.py``'s loop.
+
+One ``step()`` = one vector env step of E env copies on this rank (actors +
+Gumbel + MPE physics + replay append + episode resets, ``k_rollout``) followed
+by the update rounds the reference cadence makes due: the reference trains
+when ``train_step % 100 == 0`` with ``train_step`` counting single-env steps
+(``maddpg.py:164``, ``train.py:136``); with E copies ``train_step`` advances
+by E per vector step, so a round runs for every multiple of 100 crossed
+(E=1 is exactly the reference).  The replay-size gate (``maddpg.py:162``)
+applies unchanged.  Index draws, gathers, both optimiser steps and Polyak
+updates run on the device in the reference's agent order.
+"""
+import numpy as np
+import torch
+
+from . import envs
+from .engine import Engine
+from .parallel import EngineOps, make_allreduce, strict_round
+
+
+class VecRunner:
+    def __init__(self, scenario="simple_spread", num_envs=1024, *, n_agents=None, scenario_adversaries=None,
+                 num_adversaries=0, good_policy="maddpg", adv_policy="maddpg", batch_size=1024,
+                 num_units=64, lr=1e-2, gamma=0.95, max_episode_len=25, capacity=int(1e6), seed=0,
+                 train_every=100, world_size=1, rank=0, device=None):
+        sp = envs.spec(scenario, n_agents, scenario_adversaries)
+        self.spec = sp
+        n = sp.n_agents
+        n_adv_pol = min(n, num_adversaries)                  # train.py:84
+        local_q = [(adv_policy == "ddpg") if i < n_adv_pol else (good_policy == "ddpg") for i in range(n)]
+        self.eng = Engine(sp.obs_dims, local_q, num_units=num_units, batch_size=batch_size,
+                          max_episode_len=max_episode_len, capacity=capacity, num_envs=num_envs,
+                          scenario=scenario, num_adversaries=sp.num_adversaries, lr=lr, gamma=gamma,
+                          seed=seed * 1000003 + 17, world_size=world_size, rank=rank, device=device)
+        self.eng.init_params(seed)                           # identical replicas on every rank
+        self.eng.seed_py_random(seed + rank)                 # per-rank index stream
+        self.eng.env_reset()
+        self.n = n
+        self.num_envs = num_envs
+        self.batch_size = batch_size
+        self.gate = batch_size * max_episode_len
+        self.train_every = train_every
+        self.world_size = world_size
+        self.train_step = 0
+        self.rounds = 0
+        self._ops = EngineOps(self.eng) if world_size > 1 else None
+        self._allreduce = make_allreduce(self.eng.stream) if world_size > 1 else None
+
+    def rollout(self):
+        self.eng.env_step()
+        self.train_step += self.num_envs
+
+    def due_rounds(self, t_before, t_after):
+        if self.eng.buffer_len() < self.gate:
+            return 0
+        return t_after // self.train_every - t_before // self.train_every
+
+    def train_round(self):
+        if self.world_size == 1:
+            self.eng.update_round()
+        else:
+            strict_round(self._ops, self.n, self.world_size, self._allreduce)
+        self.rounds += 1
+
+    def step(self):
+        t0 = self.train_step
+        self.rollout()
+        k = self.due_rounds(t0, self.train_step)
+        for _ in range(k):
+            self.train_round()
+        return k
+
+    def prefill(self):
+        """vector steps without training until the replay gate opens (train.py warm-up)."""
+        while self.eng.buffer_len() < self.gate:
+            self.rollout()
+
+    def episodes(self):
+        return self.eng.episode_count()
+
+    def episode_rewards(self, first, count):
+        """[count, 1 + n]: total reward (sum over agents) then per-agent rewards."""
+        return self.eng.episode_log(first, count)
+
+    def stats(self, agent):
+        return self.eng.stats(agent)
+
+    def synchronize(self):
+        self.eng.synchronize()
+
+
+def mean_last(runner, k):
+    n = runner.episodes()
+    k = min(k, n, runner.eng.episode_log_capacity() if hasattr(runner.eng, "episode_log_capacity") else k)
+    if k <= 0:
+        return float("nan"), [float("nan")] * runner.n
+    log = runner.episode_rewards(n - k, k)
+    return float(np.mean(log[:, 0])), [float(x) for x in log[:, 1:].mean(0)]
+
+
+def to_host(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)

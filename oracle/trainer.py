@@ -56,59 +56,75 @@ def update(agents, i, buffers, idx, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
     agent j.  Returns the 6 stats and mutates agents[i] params in place.
     """
     n = len(agents)
-    ag = agents[i]
-    obs_n, act_n, obs_next_n = [], [], []
-    for j in range(n):                              # :173-177
-        o, a, _r, on, _d = buffers[j]
-        obs_n.append(o[idx].astype(F32))
-        act_n.append(a[idx].astype(F32))
-        obs_next_n.append(on[idx].astype(F32))
-    rew = buffers[i][2][idx].astype(np.float64)      # :178
-    done = buffers[i][4][idx].astype(np.float64)
-    B = len(idx)
+    batch_n = [tuple(x[idx] for x in buffers[j]) for j in range(n)]   # :173-178
+    return update_batch(agents, i, batch_n, u_tgt, u_act, gamma, grad_clip)
 
-    # ---- train q network (:180-188)
+
+def critic_grads(agents, i, batch_n, u_tgt, gamma=0.95):
+    """maddpg.py:180-188 up to the raw (unclipped) critic gradients."""
+    n = len(agents)
+    ag = agents[i]
+    obs_n = [b[0].astype(F32) for b in batch_n]
+    act_n = [b[1].astype(F32) for b in batch_n]
+    obs_next_n = [b[3].astype(F32) for b in batch_n]
+    rew = np.asarray(batch_n[i][2], np.float64)
+    done = np.asarray(batch_n[i][4], np.float64)
+    B = len(rew)
     tgt_act_n = [target_act(agents[j], obs_next_n[j], u_tgt[j]) for j in range(n)]
     xq_t = critic_input(obs_next_n, tgt_act_n, i, ag.local_q)
     target_q_next = nets.mlp_fwd(ag.tgt_critic, xq_t)[0][:, 0]
-    target_q = rew + gamma * (1.0 - done) * target_q_next.astype(np.float64)
-    y = target_q.astype(F32)
-
+    target_q = rew + gamma * (1.0 - done) * target_q_next.astype(np.float64)   # :186 (fp64)
+    y = target_q.astype(F32)                                                     # :83 fp32 placeholder
     xq = critic_input(obs_n, act_n, i, ag.local_q)
     q, cache = nets.mlp_fwd(ag.critic, xq)
     q = q[:, 0]
-    q_loss = np.mean((q.astype(np.float64) - y.astype(np.float64)) ** 2)
+    q_loss = np.mean((q.astype(np.float64) - y.astype(np.float64)) ** 2)     # :91
     dq = ((F32(2) * (q - y)) * F32(1.0 / B)).astype(F32)[:, None]
-    gq = nets.mlp_bwd(ag.critic, cache, dq)
-    gq = {k: nets.clip_by_norm(v, grad_clip) for k, v in gq.items()}
-    ag.opt_critic.apply(ag.critic, gq)
+    g = nets.mlp_bwd(ag.critic, cache, dq)
+    stats = {"q_loss": float(q_loss), "target_q": target_q, "rew": rew, "target_q_next": target_q_next}
+    return g, stats
 
-    # ---- train p network (:190-191; loss :46-56)
+
+def actor_grads(agents, i, batch_n, u_act, actor_reg=1e-3):
+    """maddpg.py:37-58 raw actor gradients (critic = its current, post-step weights)."""
+    ag = agents[i]
+    obs_n = [b[0].astype(F32) for b in batch_n]
+    act_n = [b[1].astype(F32) for b in batch_n]
+    B = obs_n[0].shape[0]
     logits, pcache = nets.mlp_fwd(ag.actor, obs_n[i])
-    a_i = nets.gumbel_softmax(logits, u_act)
+    a_i = nets.gumbel_softmax(logits, u_act)                      # :49 fresh sample
     act_in = list(act_n)
     act_in[i] = a_i
     xp = critic_input(obs_n, act_in, i, ag.local_q)
     qp, qcache = nets.mlp_fwd(ag.critic, xp)
     qp = qp[:, 0]
     A = logits.shape[1]
-    p_reg = np.mean(logits.astype(np.float64) ** 2)
-    p_loss = -np.mean(qp.astype(np.float64)) + 1e-3 * p_reg
+    p_reg = np.mean(logits.astype(np.float64) ** 2)               # :46
+    p_loss = -np.mean(qp.astype(np.float64)) + actor_reg * p_reg   # :54-56
     dqp = np.full((B, 1), -1.0 / B, F32)
     dx = nets.input_grad(ag.critic, qcache, dqp)
     off = (obs_n[i].shape[1] if ag.local_q else sum(o.shape[1] for o in obs_n)) + \
         (0 if ag.local_q else A * i)
-    da = dx[:, off:off + A]
-    dz = nets.softmax_bwd(a_i, da)
-    dlogits = (dz + logits * F32(2e-3 / (B * A))).astype(F32)
-    gp = nets.mlp_bwd(ag.actor, pcache, dlogits)
-    gp = {k: nets.clip_by_norm(v, grad_clip) for k, v in gp.items()}
-    ag.opt_actor.apply(ag.actor, gp)
+    dz = nets.softmax_bwd(a_i, dx[:, off:off + A])
+    dlogits = (dz + logits * F32(2 * actor_reg / (B * A))).astype(F32)
+    return nets.mlp_bwd(ag.actor, pcache, dlogits), float(p_loss)
 
-    # ---- target updates (:193-194)
-    nets.polyak(ag.tgt_actor, ag.actor)
-    nets.polyak(ag.tgt_critic, ag.critic)
 
-    return [float(q_loss), float(p_loss), float(np.mean(target_q)), float(np.mean(rew)),
-            float(np.mean(target_q_next.astype(np.float64))), float(np.std(target_q))], \
-        {"grad_critic": gq, "grad_actor": gp, "y": y, "q": q}
+def apply_grads(opt, params, g, grad_clip=0.5):
+    """minimize_and_clip (tf_util.py:177-182): per-tensor clip, then Adam."""
+    opt.apply(params, {k: nets.clip_by_norm(v, grad_clip) for k, v in g.items()})
+
+
+def update_batch(agents, i, batch_n, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
+    """``update`` on already-gathered batches batch_n[j] = sample_index(idx) of agent j."""
+    ag = agents[i]
+    gq, st = critic_grads(agents, i, batch_n, u_tgt, gamma)
+    apply_grads(ag.opt_critic, ag.critic, gq, grad_clip)          # :188
+    gp, p_loss = actor_grads(agents, i, batch_n, u_act)            # :191 (post-step critic)
+    apply_grads(ag.opt_actor, ag.actor, gp, grad_clip)
+    nets.polyak(ag.tgt_actor, ag.actor)                            # :193
+    nets.polyak(ag.tgt_critic, ag.critic)                          # :194
+    tq = st["target_q"]
+    return [st["q_loss"], p_loss, float(np.mean(tq)), float(np.mean(st["rew"])),
+            float(np.mean(st["target_q_next"].astype(np.float64))), float(np.std(tq))], \
+        {"grad_critic": gq, "grad_actor": gp}
