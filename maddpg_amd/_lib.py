@@ -15,7 +15,7 @@ import re
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmaddpg_hip.so")
+LIB_PATH = os.environ.get("MDP_LIB") or os.path.join(HERE, "libmaddpg_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "maddpg_hip.h")
 
 MAX_AGENTS = 8

@@ -415,7 +415,14 @@ int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
   a.m = h->m;
   a.v = h->v;
   a.grad = h->grad;
-  a.slab = from_slab ? (net ? h->slab_c : h->slab_a) : nullptr;
+  auto chunks = [](const NDesc& d, int* blk) {
+    blk[0] = 0;
+    for (int t = 0; t < 6; ++t)
+      blk[t + 1] = blk[t] + (d.t[t].rows * d.t[t].cols + MDP_APPLY_CHUNK - 1) / MDP_APPLY_CHUNK;
+  };
+  chunks(a.net, a.blk);
+  chunks(a.other, a.oblk);
+  a.slab = nullptr;
   a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
   a.nwg = h->L.nwg;
   a.scale = scale;
@@ -443,12 +450,28 @@ int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
   return 0;
 }
 
+int do_reduce(mdp_handle* h, int agent, int net) {
+  const NDesc& d = net_of(h, agent, net);
+  ReduceArgs a;
+  a.slab = net ? h->slab_c : h->slab_a;
+  a.nwg = h->L.nwg;
+  a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
+  a.grad = h->grad;
+  a.off = d.off;
+  a.size = d.size;
+  ProfScope p(h, MDP_K_REDUCE);
+  HIPCHK(h, mdp_launch_reduce(a, h->stream));
+  return 0;
+}
+
 int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act) {
   int rc;
   if ((rc = do_critic_grad(h, agent, idx, u_tgt))) return rc;
-  if ((rc = do_apply(h, agent, 1, true, 1.0f))) return rc;
+  if ((rc = do_reduce(h, agent, 1))) return rc;
+  if ((rc = do_apply(h, agent, 1, false, 1.0f))) return rc;
   if ((rc = do_actor_grad(h, agent, idx, u_act))) return rc;
-  if ((rc = do_apply(h, agent, 0, true, 1.0f))) return rc;
+  if ((rc = do_reduce(h, agent, 0))) return rc;
+  if ((rc = do_apply(h, agent, 0, false, 1.0f))) return rc;
   return 0;
 }
 
@@ -824,17 +847,7 @@ int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const f
 
 int mdp_reduce_grad(mdp_handle* h, int32_t agent, int32_t net) {
   if (bad_agent(h, agent)) return -1;
-  const NDesc& d = net_of(h, agent, net);
-  ReduceArgs a;
-  a.slab = net ? h->slab_c : h->slab_a;
-  a.nwg = h->L.nwg;
-  a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
-  a.grad = h->grad;
-  a.off = d.off;
-  a.size = d.size;
-  ProfScope p(h, MDP_K_REDUCE);
-  HIPCHK(h, mdp_launch_reduce(a, h->stream));
-  return 0;
+  return do_reduce(h, agent, net ? 1 : 0);
 }
 
 int mdp_apply_grad(mdp_handle* h, int32_t agent, int32_t net, float scale) {

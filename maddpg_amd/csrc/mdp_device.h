@@ -20,6 +20,19 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// diagnostic build only (-DMDP_STAMPS): wall-clock stamps of workgroup 0
+#ifdef MDP_STAMPS
+__device__ unsigned long long g_mdp_stamps[64];
+#define MDP_STAMP(i)                                                                     \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_mdp_stamps[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define MDP_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------ RNG
 struct Philox {
   __device__ static inline uint4 round(uint4 c, uint2 k) {
@@ -83,6 +96,41 @@ __host__ __device__ inline int lds_ld(int cols) { return (cols | 1); }
 // ------------------------------------------------------ MFMA layer tiles
 // Y[16][N] = act(X[16][K] @ W[K][N] + b)   X,Y in LDS; W,b global row-major [K][N]
 // N multiple of 16.  Column tiles are dealt round-robin over the 4 waves.
+// B fragments of one 64-deep K chunk (16 MFMA k-steps) for one column: all 16
+// global loads are issued together so the chunk pays one L2 latency, not 16.
+#define MDP_KC 16
+__device__ inline void load_wchunk(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
+                                   int K, int kq) {
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    const int k = c0 + 4 * s + kq;
+    w[s] = k < K ? W[k * ldw + col] : 0.f;
+  }
+}
+// same for a transposed operand: element (k, col) at W[col * ldw + k]
+__device__ inline void load_wchunk_t(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
+                                     int K, int kq, bool colok) {
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    const int k = c0 + 4 * s + kq;
+    w[s] = (k < K && colok) ? W[col * ldw + k] : 0.f;
+  }
+}
+// acc += A[r][c0 .. c0+63] . w  with A from LDS (row r = lane&15)
+__device__ inline f32x4 mfma_chunk(f32x4 acc, const float (&w)[MDP_KC], const float* A, int lda, int r, int c0,
+                                   int K, int kq) {
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    const int k0 = c0 + 4 * s;
+    if (k0 < K) {  // wave-uniform
+      const int k = k0 + kq;
+      const float a = k < K ? A[r * lda + k] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[s], acc, 0, 0, 0);
+    }
+  }
+  return acc;
+}
+
 template <bool RELU>
 __device__ inline void tile_fwd(const float* X, int ldx, int K, const float* __restrict__ W,
                                 const float* __restrict__ b, int N, float* Y, int ldy) {
@@ -91,12 +139,16 @@ __device__ inline void tile_fwd(const float* X, int ldx, int K, const float* __r
   for (int nt = wave; nt < (N >> 4); nt += MDP_NW) {
     const int col = nt * 16 + r;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < K; k0 += 4) {
-      const int k = k0 + kq;
-      const bool in = k < K;
-      const float a = in ? X[r * ldx + k] : 0.f;
-      const float w = in ? W[k * N + col] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, acc, 0, 0, 0);
+    float wa[MDP_KC], wb[MDP_KC];
+    load_wchunk(wa, W, N, col, 0, K, kq);
+    for (int c0 = 0; c0 < K; c0 += 4 * MDP_KC) {
+      const bool more = c0 + 4 * MDP_KC < K;
+      if (more) load_wchunk(wb, W, N, col, c0 + 4 * MDP_KC, K, kq);
+      acc = mfma_chunk(acc, wa, X, ldx, r, c0, K, kq);
+      if (more) {
+#pragma unroll
+        for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+      }
     }
     const float bias = b[col];
 #pragma unroll
@@ -143,10 +195,16 @@ __device__ inline void tile_dgrad_relu(const float* dY, int ldy, int N, const fl
   for (int nt = wave; nt < (K >> 4); nt += MDP_NW) {
     const int kk = nt * 16 + r;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int n0 = 0; n0 < N; n0 += 4) {
-      const float a = dY[r * ldy + n0 + kq];
-      const float w = W[kk * N + n0 + kq];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w, acc, 0, 0, 0);
+    float wa[MDP_KC], wb[MDP_KC];
+    load_wchunk_t(wa, W, N, kk, 0, N, kq, true);
+    for (int c0 = 0; c0 < N; c0 += 4 * MDP_KC) {
+      const bool more = c0 + 4 * MDP_KC < N;
+      if (more) load_wchunk_t(wb, W, N, kk, c0 + 4 * MDP_KC, N, kq, true);
+      acc = mfma_chunk(acc, wa, dY, ldy, r, c0, N, kq);
+      if (more) {
+#pragma unroll
+        for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

@@ -46,8 +46,11 @@ struct ReduceArgs {
   int64_t off, size;
 };
 
+#define MDP_APPLY_CHUNK 1024  // parameters per apply workgroup
+
 struct ApplyArgs {
   NDesc net, other;
+  int blk[7], oblk[7];  // prefix counts of chunk workgroups per tensor (net / other)
   float* theta;
   float* target;
   float* m;

@@ -247,8 +247,11 @@ __global__ __launch_bounds__(MDP_NT) void k_critic_grad(CriticArgs a) {
   const int nvalid = min(MDP_R, a.B - r0);
   const bool lq = ag.local_q != 0;
   const uint32_t ctr = a.ctl->upd_ctr;
+  MDP_STAMP(0);
 
   gather_tile(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+  __syncthreads();
+  MDP_STAMP(1);
   __syncthreads();
 
   // target critic input: [obs'_all | a~_all] (global) or [obs'_i | a~_i] (local)
@@ -273,11 +276,14 @@ __global__ __launch_bounds__(MDP_NT) void k_critic_grad(CriticArgs a) {
       for (int k = 0; k < MDP_ACT_DIM; ++k) xt[tid * ldc + dst + k] = act[k];
     }
     __syncthreads();
+    MDP_STAMP(2 + j);
   }
 
+  MDP_STAMP(9);
   // target critic -> Q'(o', a~)
   mlp_fwd_tile<H>(xt, ldc, ag.cin, a.target, ag.critic, h1, h2, ldh, qt, 1);
 
+  MDP_STAMP(10);
   // critic forward on (obs_n, act_n): the row's prefix (global) or [obs_i | act_i]
   const float* X = rowbuf;
   int ldX = ldr;
@@ -290,6 +296,7 @@ __global__ __launch_bounds__(MDP_NT) void k_critic_grad(CriticArgs a) {
   }
   mlp_fwd_tile<H>(X, ldX, ag.cin, a.theta, ag.critic, h1c, h2c, ldh, qv, 1);
 
+  MDP_STAMP(11);
   // TD target (fp64, maddpg.py:186), loss partials, dL/dq = 2(q - y)/B
   double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;
   if (tid < MDP_R) {
@@ -323,6 +330,7 @@ __global__ __launch_bounds__(MDP_NT) void k_critic_grad(CriticArgs a) {
   }
   __syncthreads();
 
+  MDP_STAMP(12);
   // backward through the critic (tf.gradients of q_loss w.r.t. q_func vars)
   const NDesc& nd = ag.critic;
   const float* W3 = a.theta + nd.t[4].off;
@@ -346,8 +354,11 @@ __global__ __launch_bounds__(MDP_NT) void k_critic_grad(CriticArgs a) {
   colsum_store(d2, ldh, H, slab + nd.t[3].off);
   tile_dgrad_relu(d2, ldh, H, a.theta + nd.t[2].off, H, h1c, ldh, d1, ldh);
   __syncthreads();
+  MDP_STAMP(13);
   tile_wgrad(X, ldX, ag.cin, d1, ldh, H, slab + nd.t[0].off);
   colsum_store(d1, ldh, H, slab + nd.t[1].off);
+  __syncthreads();
+  MDP_STAMP(14);
 }
 
 // One agent's actor step gradients (maddpg.py:37-58): actor forward, fresh
@@ -514,41 +525,45 @@ __device__ inline bool last_block(uint32_t* ticket) {
 }
 }  // namespace
 
-// Reduce per-workgroup partials of one net into grad[] (fixed order -> deterministic).
+// grad[e] = sum_w slab[w][e] in fixed w order (deterministic); one element per
+// thread, the nwg partial loads unrolled 8-wide so they are in flight together.
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs a) {
-  const int64_t n = a.size;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int w = 0; w < a.nwg; ++w) s += a.slab[(int64_t)w * a.slab_stride + e];
-    a.grad[a.off + e] = s;
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= a.size) return;
+  const float* p = a.slab + e;
+  float s = 0.f;
+  int w = 0;
+  for (; w + 8 <= a.nwg; w += 8) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = p[(int64_t)(w + q) * a.slab_stride];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
   }
+  for (; w < a.nwg; ++w) s += p[(int64_t)w * a.slab_stride];
+  a.grad[a.off + e] = s;
 }
 
-// blocks 0..5: tensor b of `net`: reduce partials (or read grad), scale,
-// per-tensor clip_by_norm, TF1 ApplyAdam, optional Polyak of that tensor;
-// blocks 6..11 (polyak): Polyak of `other`'s tensors; last block: stats.
-// The last block to finish also advances this optimizer's beta powers.
+// Workgroup (tensor t, chunk c) of `net`: per-tensor clip_by_norm (norm of the
+// whole scaled tensor, recomputed by every chunk from the reduced gradient),
+// TF1 ApplyAdam on the chunk, optional Polyak of the chunk; then Polyak chunks
+// of `other` (actor step only) and one stats workgroup.  The last workgroup to
+// finish advances this optimizer's beta powers.
 __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
   __shared__ double red[4];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const float b1p = a.beta[0], b2p = a.beta[1];
-  if (b < 6) {
-    const TDesc td = a.net.t[b];
+  if (b < a.blk[6]) {
+    int t = 0;
+    while (b >= a.blk[t + 1]) ++t;
+    const TDesc td = a.net.t[t];
     const int n = td.rows * td.cols;
-    const int rel = td.off - a.net.off;
+    const float* g = a.grad + td.off;
     double ss = 0.0;
     for (int e = tid; e < n; e += blockDim.x) {
-      float g;
-      if (a.slab) {
-        g = 0.f;
-        for (int w = 0; w < a.nwg; ++w) g += a.slab[(int64_t)w * a.slab_stride + rel + e];
-      } else {
-        g = a.grad[td.off + e];
-      }
-      g = g * a.scale;
-      a.grad[td.off + e] = g;
-      ss += (double)g * (double)g;
+      const float v = g[e] * a.scale;
+      ss += (double)v * (double)v;
     }
     ss = block_sum_d(ss, red);
     const float norm = (float)sqrt(ss);
@@ -557,26 +572,33 @@ __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
     const float one = 1.0f;
     const float alpha = a.lr * sqrtf(one - b2p) / (one - b1p);
     const float c1 = one - a.b1, c2 = one - a.b2;
-    for (int e = tid; e < n; e += blockDim.x) {
+    const int e0 = (b - a.blk[t]) * MDP_APPLY_CHUNK;
+    const int e1 = min(n, e0 + MDP_APPLY_CHUNK);
+    for (int e = e0 + tid; e < e1; e += blockDim.x) {
       const int64_t i = td.off + e;
-      const float g = (a.grad[i] * clip) / denom;
-      const float m = a.m[i] + (g - a.m[i]) * c1;
-      const float v = a.v[i] + (g * g - a.v[i]) * c2;
+      const float gc = ((g[e] * a.scale) * clip) / denom;
+      const float m = a.m[i] + (gc - a.m[i]) * c1;
+      const float v = a.v[i] + (gc * gc - a.v[i]) * c2;
       const float th = a.theta[i] - (m * alpha) / (sqrtf(v) + a.eps);
       a.m[i] = m;
       a.v[i] = v;
       a.theta[i] = th;
       if (a.polyak) a.target[i] = a.pa * a.target[i] + a.pb * th;
     }
-  } else if (a.polyak && b < 12) {
-    const TDesc td = a.other.t[b - 6];
+  } else if (a.polyak && b < a.blk[6] + a.oblk[6]) {
+    const int bb = b - a.blk[6];
+    int t = 0;
+    while (bb >= a.oblk[t + 1]) ++t;
+    const TDesc td = a.other.t[t];
     const int n = td.rows * td.cols;
-    for (int e = tid; e < n; e += blockDim.x) {
+    const int e0 = (bb - a.oblk[t]) * MDP_APPLY_CHUNK;
+    const int e1 = min(n, e0 + MDP_APPLY_CHUNK);
+    for (int e = e0 + tid; e < e1; e += blockDim.x) {
       const int64_t i = td.off + e;
       a.target[i] = a.pa * a.target[i] + a.pb * a.theta[i];
     }
   } else if (a.stats_mode) {
-    // stats block (maddpg.py:196): critic fills 0,2,3,4,5; actor fills 1
+    // stats workgroup (maddpg.py:196): critic fills 0,2,3,4,5; actor fills 1
     if (a.stats_mode == 1) {
       double sl = 0.0, sy = 0.0, sr = 0.0, sq = 0.0;
       if (tid == 0) {
@@ -1145,7 +1167,7 @@ hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t 
   return H == 64 ? launch_eval_t<64>(a, lds_bytes, s) : launch_eval_t<128>(a, lds_bytes, s);
 }
 hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s) {
-  const int grid = 6 + (a.polyak ? 6 : 0) + (a.stats_mode ? 1 : 0);
+  const int grid = a.blk[6] + (a.polyak ? a.oblk[6] : 0) + (a.stats_mode ? 1 : 0);
   hipLaunchKernelGGL(k_apply, dim3(grid), dim3(256), 0, s, a);
   MDP_CHECK_LAUNCH();
   return hipSuccess;
@@ -1213,3 +1235,9 @@ hipError_t mdp_launch_set_ring(Ctl* ctl, int64_t len, int64_t next, hipStream_t 
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
+
+#ifdef MDP_STAMPS
+extern "C" int mdp_debug_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif
