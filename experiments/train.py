@@ -1,0 +1,148 @@
+"""MADDPG training on MI355X -- drop-in for the reference's ``experiments/train.py``.
+
+Same flags, defaults and console lines as ``experiments/train.py:11-189``.
+The loop runs on the device (``maddpg_amd.runner.VecRunner``): E copies of the
+MPE scenario step per launch, experience goes straight into the device
+replay, and every agent's ``update()`` runs in the reference's order at the
+reference cadence (one round per 100 transitions; with E=1 -- the default --
+this is exactly the reference loop).  Extra flags: ``--num-envs``, ``--seed``,
+``--num-agents``/``--scenario-adversaries`` (scenario size), ``--train-every``.
+
+Episode accounting follows the reference exactly: ``len(episode_rewards)`` is
+the number of finished episodes + 1 (a new 0 entry is appended at every reset,
+``train.py:127-133``), the progress line is printed when that length is a
+multiple of ``--save-rate`` and averages the last ``--save-rate`` entries
+(including the fresh 0), and training stops once it exceeds
+``--num-episodes``.  Every env copy terminates at ``--max-episode-len`` steps
+(MPE scenarios have no done callback), so the episode count is known on the
+host without a device sync.
+
+    python experiments/train.py --scenario simple_spread --num-envs 1024 --exp-name spread
+    torchrun --nproc-per-node 8 experiments/train.py --scenario simple_spread --num-envs 4096
+"""
+import argparse
+import os
+import pickle
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def parse_args(argv=None):
+    parser = argparse.ArgumentParser("Reinforcement Learning experiments for multiagent environments")
+    # Environment
+    parser.add_argument("--scenario", type=str, default="simple", help="name of the scenario script")
+    parser.add_argument("--max-episode-len", type=int, default=25, help="maximum episode length")
+    parser.add_argument("--num-episodes", type=int, default=60000, help="number of episodes")
+    parser.add_argument("--num-adversaries", type=int, default=0, help="number of adversaries")
+    parser.add_argument("--good-policy", type=str, default="maddpg", help="policy for good agents")
+    parser.add_argument("--adv-policy", type=str, default="maddpg", help="policy of adversaries")
+    # Core training parameters
+    parser.add_argument("--lr", type=float, default=1e-2, help="learning rate for Adam optimizer")
+    parser.add_argument("--gamma", type=float, default=0.95, help="discount factor")
+    parser.add_argument("--batch-size", type=int, default=1024, help="number of episodes to optimize at the same time")
+    parser.add_argument("--num-units", type=int, default=64, help="number of units in the mlp")
+    # Checkpointing
+    parser.add_argument("--exp-name", type=str, default=None, help="name of the experiment")
+    parser.add_argument("--save-dir", type=str, default="/tmp/policy/", help="directory in which training state and model should be saved")
+    parser.add_argument("--save-rate", type=int, default=1000, help="save model once every time this many episodes are completed")
+    parser.add_argument("--load-dir", type=str, default="", help="directory in which training state and model are loaded")
+    # Evaluation
+    parser.add_argument("--restore", action="store_true", default=False)
+    parser.add_argument("--display", action="store_true", default=False)
+    parser.add_argument("--benchmark", action="store_true", default=False)
+    parser.add_argument("--benchmark-iters", type=int, default=100000, help="number of iterations run for benchmarking")
+    parser.add_argument("--benchmark-dir", type=str, default="./benchmark_files/", help="directory where benchmark data is saved")
+    parser.add_argument("--plots-dir", type=str, default="./learning_curves/", help="directory where plot data is saved")
+    # MI355X build extensions
+    parser.add_argument("--num-envs", type=int, default=1, help="env copies stepped together per GPU")
+    parser.add_argument("--seed", type=int, default=0, help="seed of weights, index stream and device RNG")
+    parser.add_argument("--num-agents", type=int, default=None, help="scenario agent count override")
+    parser.add_argument("--scenario-adversaries", type=int, default=None, help="adversaries in the scenario world")
+    parser.add_argument("--train-every", type=int, default=100, help="transitions per update round (maddpg.py:164)")
+    return parser.parse_args(argv)
+
+
+def train(arglist):
+    import torch
+
+    from maddpg_amd.parallel import init_process_group_from_env
+    from maddpg_amd.runner import VecRunner
+
+    if arglist.display:
+        raise SystemExit("--display needs MPE's pyglet viewer, which this build does not ship")
+    if arglist.benchmark:
+        raise SystemExit("--benchmark (scenario benchmark_data) is not implemented in this round")
+    exp_name = arglist.exp_name if arglist.exp_name is not None else arglist.scenario
+    world, rank, local = init_process_group_from_env()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    runner = VecRunner(arglist.scenario, arglist.num_envs, n_agents=arglist.num_agents,
+                       scenario_adversaries=arglist.scenario_adversaries,
+                       num_adversaries=arglist.num_adversaries, good_policy=arglist.good_policy,
+                       adv_policy=arglist.adv_policy, batch_size=arglist.batch_size,
+                       num_units=arglist.num_units, lr=arglist.lr, gamma=arglist.gamma,
+                       max_episode_len=arglist.max_episode_len, seed=arglist.seed,
+                       train_every=arglist.train_every, world_size=world, rank=rank)
+    n = runner.n
+    num_adversaries = min(n, arglist.num_adversaries)
+    say = (lambda *a: print(*a, flush=True)) if rank == 0 else (lambda *a: None)
+    say('Using good policy {} and adv policy {}'.format(arglist.good_policy, arglist.adv_policy))
+
+    if arglist.load_dir == "":
+        arglist.load_dir = arglist.save_dir
+    if arglist.restore:
+        say('Loading previous state...')
+        runner.eng.load_state(arglist.load_dir)
+
+    E, L = arglist.num_envs, arglist.max_episode_len
+    final_ep_rewards, final_ep_ag_rewards = [], []
+    t_start = time.time()
+    vec_steps = 0
+    finished = 0                       # finished episodes on this rank
+    say('Starting iterations...')
+    while True:
+        runner.step()
+        vec_steps += 1
+        if vec_steps % L:
+            continue
+        # every env copy just terminated (train.py:116,127): E new episodes
+        prev = finished
+        finished += E
+        length_before, length_after = prev + 1, finished + 1   # len(episode_rewards)
+        k = length_after // arglist.save_rate - length_before // arglist.save_rate
+        if k > 0 and rank == 0:
+            runner.eng.save_state(arglist.save_dir)
+            # np.mean(episode_rewards[-save_rate:]) with the fresh 0 entry included
+            m = min(arglist.save_rate - 1, finished)
+            log = runner.episode_rewards(finished - m, m) if m > 0 else np.zeros((0, 1 + n), np.float32)
+            mean_ep = float(np.sum(log[:, 0], dtype=np.float64) / arglist.save_rate)
+            mean_ag = [float(np.sum(log[:, 1 + j], dtype=np.float64) / arglist.save_rate) for j in range(n)]
+            steps = vec_steps * E
+            if num_adversaries == 0:
+                print("steps: {}, episodes: {}, mean episode reward: {}, time: {}".format(
+                    steps, length_after, mean_ep, round(time.time() - t_start, 3)), flush=True)
+            else:
+                print("steps: {}, episodes: {}, mean episode reward: {}, agent episode reward: {}, time: {}".format(
+                    steps, length_after, mean_ep, mean_ag, round(time.time() - t_start, 3)), flush=True)
+            t_start = time.time()
+            final_ep_rewards.append(mean_ep)
+            final_ep_ag_rewards.extend(mean_ag)
+        if length_after > arglist.num_episodes:
+            if rank == 0:
+                os.makedirs(arglist.plots_dir, exist_ok=True)
+                with open(arglist.plots_dir + exp_name + '_rewards.pkl', 'wb') as fp:
+                    pickle.dump(final_ep_rewards, fp)
+                with open(arglist.plots_dir + exp_name + '_agrewards.pkl', 'wb') as fp:
+                    pickle.dump(final_ep_ag_rewards, fp)
+            say('...Finished total of {} episodes.'.format(length_after))
+            break
+    runner.synchronize()
+    return runner
+
+
+if __name__ == '__main__':
+    train(parse_args())

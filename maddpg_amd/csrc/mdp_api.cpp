@@ -188,7 +188,7 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   sz[MDP_R_STATS] = 8 * 8 * (int64_t)n;
   sz[MDP_R_ENV] = (int64_t)E * (4 * 4 * L.n_ent + 4 + 4 + 4 * n) + 64;
   sz[MDP_R_EPLOG] = 4 * (int64_t)L.eplog_rows * (1 + n);
-  sz[MDP_R_BETA] = 4 * 4 * (int64_t)n;
+  sz[MDP_R_BETA] = 4 * 8 * (int64_t)n;  // per optimizer: next powers (TF vars), powers of this step
   sz[MDP_R_SLAB] = 4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg + 8 * (int64_t)c->batch_size + 256;
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
@@ -431,7 +431,7 @@ int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
   a.b1 = h->cfg.adam_b1;
   a.b2 = h->cfg.adam_b2;
   a.eps = h->cfg.adam_eps;
-  a.beta = h->beta + agent * 4 + net * 2;
+  a.beta = h->beta + agent * 8 + net * 4;
   a.polyak = net ? 0 : 1;
   const double tau = (double)h->cfg.tau;
   a.pa = (float)(1.0 - tau);
@@ -459,6 +459,11 @@ int do_reduce(mdp_handle* h, int agent, int net) {
   a.grad = h->grad;
   a.off = d.off;
   a.size = d.size;
+  a.beta = h->beta + agent * 8 + net * 4;
+  a.b1 = h->cfg.adam_b1;
+  a.b2 = h->cfg.adam_b2;
+  a.ctl = h->ctl;
+  a.bump_ctr = net ? 0 : 1;
   ProfScope p(h, MDP_K_REDUCE);
   HIPCHK(h, mdp_launch_reduce(a, h->stream));
   return 0;
@@ -563,10 +568,10 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->y = (double*)p;
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
-  std::vector<float> beta(4 * cfg->n_agents);
-  for (int i = 0; i < cfg->n_agents * 2; ++i) {
-    beta[2 * i] = cfg->adam_b1;
-    beta[2 * i + 1] = cfg->adam_b2;
+  std::vector<float> beta(8 * cfg->n_agents);
+  for (int i = 0; i < cfg->n_agents * 2; ++i) {  // TF1: beta powers start at beta
+    beta[4 * i] = beta[4 * i + 2] = cfg->adam_b1;
+    beta[4 * i + 1] = beta[4 * i + 3] = cfg->adam_b2;
   }
   HIPCHK(h, hipMemcpyAsync(h->beta, beta.data(), 4 * beta.size(), hipMemcpyHostToDevice, h->stream));
   Ctl c;
@@ -664,14 +669,14 @@ int mdp_get_params(mdp_handle* h, int32_t agent, int32_t which, float* dst, int6
 
 int mdp_get_beta_powers(mdp_handle* h, int32_t agent, int32_t net, float out2[2]) {
   if (bad_agent(h, agent)) return -1;
-  HIPCHK(h, hipMemcpyAsync(out2, h->beta + agent * 4 + (net ? 2 : 0), 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(out2, h->beta + agent * 8 + (net ? 4 : 0), 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return 0;
 }
 
 int mdp_set_beta_powers(mdp_handle* h, int32_t agent, int32_t net, const float in2[2]) {
   if (bad_agent(h, agent)) return -1;
-  HIPCHK(h, hipMemcpyAsync(h->beta + agent * 4 + (net ? 2 : 0), in2, 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->beta + agent * 8 + (net ? 4 : 0), in2, 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return 0;
 }
@@ -964,10 +969,13 @@ int64_t mdp_episode_count(mdp_handle* h) {
 
 int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out) {
   const int64_t cap = h->L.eplog_rows, w = 1 + h->cfg.n_agents;
-  if (n > cap) return fail(h, "episode log request exceeds ring");
-  for (int64_t k = 0; k < n; ++k) {
-    const int64_t slot = (first + k) % cap;
-    HIPCHK(h, hipMemcpyAsync(out + k * w, h->eplog + slot * w, 4 * w, hipMemcpyDeviceToHost, h->stream));
+  if (n > cap || first < 0) return fail(h, "episode log request exceeds ring");
+  int64_t done = 0;
+  while (done < n) {  // at most two contiguous spans of the ring
+    const int64_t slot = (first + done) % cap;
+    const int64_t span = std::min(n - done, cap - slot);
+    HIPCHK(h, hipMemcpyAsync(out + done * w, h->eplog + slot * w, 4 * w * span, hipMemcpyDeviceToHost, h->stream));
+    done += span;
   }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return 0;

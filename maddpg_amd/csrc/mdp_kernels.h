@@ -44,6 +44,10 @@ struct ReduceArgs {
   int nwg, slab_stride;
   float* grad;
   int64_t off, size;
+  float* beta;          // [4] of this optimizer: next powers (TF variables), this step's powers
+  float b1, b2;
+  Ctl* ctl;
+  int bump_ctr;         // actor phase: advance the training-noise counter
 };
 
 #define MDP_APPLY_CHUNK 1024  // parameters per apply workgroup

@@ -527,8 +527,20 @@ __device__ inline bool last_block(uint32_t* ticket) {
 
 // grad[e] = sum_w slab[w][e] in fixed w order (deterministic); one element per
 // thread, the nwg partial loads unrolled 8-wide so they are in flight together.
+// Thread 0 also advances the optimizer step (replaces the AdamOptimizer._finish
+// beta-power update): beta[2..3] <- beta[0..1] (powers this step's ApplyAdam
+// uses), beta[0..1] *= (b1, b2) in fp32.  k_reduce always precedes k_apply in
+// stream order, so no cross-workgroup protocol is needed.
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs a) {
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e == 0 && a.beta) {
+    const float p1 = a.beta[0], p2 = a.beta[1];
+    a.beta[2] = p1;
+    a.beta[3] = p2;
+    a.beta[0] = p1 * a.b1;
+    a.beta[1] = p2 * a.b2;
+    if (a.bump_ctr) a.ctl->upd_ctr += 1u;
+  }
   if (e >= a.size) return;
   const float* p = a.slab + e;
   float s = 0.f;
@@ -553,7 +565,7 @@ __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
   __shared__ double red[4];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const float b1p = a.beta[0], b2p = a.beta[1];
+  const float b1p = a.beta[2], b2p = a.beta[3];  // powers for this step, latched by k_reduce
   if (b < a.blk[6]) {
     int t = 0;
     while (b >= a.blk[t + 1]) ++t;
@@ -635,12 +647,6 @@ __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
       }
       a.stats_out[1] = -sq / a.B + (double)a.reg * (sp / ((double)a.B * MDP_ACT_DIM));
     }
-  }
-  if (last_block(a.ticket) && tid == 0) {
-    a.beta[0] = b1p * a.b1;
-    a.beta[1] = b2p * a.b2;
-    if (a.bump_ctr) a.ctl->upd_ctr += 1u;
-    *a.ticket = 0u;
   }
 }
 

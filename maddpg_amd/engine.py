@@ -8,6 +8,7 @@ the engine's stream.  No CPU fallback exists: construction raises without a
 GPU or without the built library.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -192,6 +193,50 @@ class Engine:
                 self.set_params(i, which, p)
         return H
 
+    # --------------------------------------------------------- checkpoint
+    SETS = ("actor", "critic", "tgt_actor", "tgt_critic", "m_actor", "v_actor", "m_critic", "v_critic")
+
+    def state_dict(self):
+        """Every variable tf.train.Saver would save (tf_util.py:259-273): weights,
+        targets, Adam slots and beta powers, keyed like the TF1 scopes."""
+        out = {}
+        for i in range(self.n):
+            for w in self.SETS:
+                for k, v in self.get_params(i, w).items():
+                    out[f"agent_{i}/{w}/{k}"] = v
+            out[f"agent_{i}/actor/beta_power"] = self.get_beta_powers(i, 0)
+            out[f"agent_{i}/critic/beta_power"] = self.get_beta_powers(i, 1)
+        return out
+
+    def load_state_dict(self, sd):
+        for i in range(self.n):
+            for w in self.SETS:
+                self.set_params(i, w, {k: sd[f"agent_{i}/{w}/{k}"] for k in TENSOR_NAMES})
+            self.set_beta_powers(i, 0, sd[f"agent_{i}/actor/beta_power"])
+            self.set_beta_powers(i, 1, sd[f"agent_{i}/critic/beta_power"])
+
+    @staticmethod
+    def checkpoint_path(fname):
+        if fname.endswith(".npz"):
+            return fname
+        if fname.endswith("/") or os.path.isdir(fname):
+            return os.path.join(fname, "maddpg_amd_state.npz")
+        return fname + ".npz"
+
+    def save_state(self, fname):
+        path = self.checkpoint_path(fname)
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        np.savez(path, **self.state_dict())
+        return path
+
+    def load_state(self, fname):
+        path = self.checkpoint_path(fname)
+        with np.load(path, allow_pickle=False) as z:
+            self.load_state_dict({k: z[k] for k in z.files})
+        return path
+
     # ------------------------------------------------------------- replay
     def buffer_len(self):
         return int(self.lib.mdp_buffer_len(self.h))
@@ -307,6 +352,17 @@ class Engine:
         out = (ctypes.c_double * 6)()
         self._c("mdp_get_stats", agent, out)
         return list(out)
+
+    def stats_future(self, agent):
+        """Snapshot of agent's 6 update stats, copied D2H in stream order (no sync);
+        returns (host tensor, event) -- wait on the event before reading."""
+        src = self.region("stats", torch.float64)[agent * 8:agent * 8 + 6]
+        dst = torch.empty(6, dtype=torch.float64, pin_memory=True)
+        with torch.cuda.stream(self.stream):
+            dst.copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return dst, ev
 
     # ----------------------------------------------------------------- env
     @property

@@ -10,12 +10,15 @@ by E per vector step, so a round runs for every multiple of 100 crossed
 applies unchanged.  Index draws, gathers, both optimiser steps and Polyak
 updates run on the device in the reference's agent order.
 """
-import numpy as np
-import torch
-
 from . import envs
 from .engine import Engine
 from .parallel import EngineOps, make_allreduce, strict_round
+
+
+def rounds_due(t_before, t_after, every=100):
+    """update rounds for train_step going t_before -> t_after: one per multiple of
+    `every` crossed (maddpg.py:164 ``t % 100 == 0`` checked at every t)."""
+    return t_after // every - t_before // every
 
 
 class VecRunner:
@@ -53,7 +56,7 @@ class VecRunner:
     def due_rounds(self, t_before, t_after):
         if self.eng.buffer_len() < self.gate:
             return 0
-        return t_after // self.train_every - t_before // self.train_every
+        return rounds_due(t_before, t_after, self.train_every)
 
     def train_round(self):
         if self.world_size == 1:
@@ -87,16 +90,3 @@ class VecRunner:
 
     def synchronize(self):
         self.eng.synchronize()
-
-
-def mean_last(runner, k):
-    n = runner.episodes()
-    k = min(k, n, runner.eng.episode_log_capacity() if hasattr(runner.eng, "episode_log_capacity") else k)
-    if k <= 0:
-        return float("nan"), [float("nan")] * runner.n
-    log = runner.episode_rewards(n - k, k)
-    return float(np.mean(log[:, 0])), [float(x) for x in log[:, 1:].mean(0)]
-
-
-def to_host(t):
-    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)

@@ -1,0 +1,120 @@
+"""``MADDPGAgentTrainer`` drop-in (``maddpg/trainer/maddpg.py:112-196``).
+
+Same constructor, methods, attributes and return values.  Every trainer built
+in one session shares one device engine (see ``common/tf_util.py``); its
+``update`` runs on the GPU in the reference's order: gates (``:162-165``),
+``make_index`` from the global ``random`` stream (``:167``), gather of every
+agent's buffer with that index (``:173-178``, fused into the grad kernels),
+target actors + target critic + fp64 TD target (``:180-187``), critic step
+(``:188``), actor step against the updated critic (``:191``), Polyak actor
+then critic (``:193-194``).  ``update`` returns the 6 stats of ``:196`` as a
+lazy sequence that synchronises only when read.
+
+``model`` is accepted for signature parity: the network is the reference's
+``mlp_model`` (2 hidden ReLU layers of ``args.num_units``, ``train.py:39-46``).
+"""
+import numpy as np
+import torch
+
+from .. import AgentTrainer
+from ..common import tf_util as U
+from .replay_buffer import ReplayBuffer
+
+
+class UpdateStats(object):
+    """[q_loss, p_loss, mean(target_q), mean(rew), mean(target_q_next), std(target_q)]."""
+
+    def __init__(self, engine, agent):
+        self._host, self._event = engine.stats_future(agent)
+        self._vals = None
+
+    def _get(self):
+        if self._vals is None:
+            self._event.synchronize()
+            self._vals = [float(x) for x in self._host.tolist()]
+        return self._vals
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    def __len__(self):
+        return 6
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __eq__(self, other):
+        return list(self._get()) == list(other)
+
+    def __repr__(self):
+        return repr(list(self._get()))
+
+    def tolist(self):
+        return list(self._get())
+
+
+class MADDPGAgentTrainer(AgentTrainer):
+    def __init__(self, name, model, obs_shape_n, act_space_n, agent_index, args, local_q_func=False):
+        self.name = name
+        self.n = len(obs_shape_n)
+        self.agent_index = agent_index
+        self.args = args
+        self.obs_shape_n = [tuple(s) for s in obs_shape_n]
+        self.act_space_n = act_space_n
+        self.local_q_func = local_q_func
+        for sp in act_space_n:
+            if getattr(sp, "n", 5) != 5:
+                raise NotImplementedError("only Discrete(5) MPE action spaces are supported")
+        self.session = U.get_session()
+        self.session.register(self)
+        self.replay_buffer = ReplayBuffer(1e6, _session=self.session, _agent=agent_index)
+        self.max_replay_buffer_len = args.batch_size * args.max_episode_len
+        self.replay_sample_index = None
+        i = agent_index
+        self.p_debug = {"p_values": lambda obs: self._eng().actor_logits(i, self._t(obs)).cpu().numpy(),
+                        "target_act": lambda obs: self._eng().act(i, self._t(obs), target=True).cpu().numpy()}
+        self.q_debug = {"q_values": lambda *a: self._q(a, False), "target_q_values": lambda *a: self._q(a, True)}
+
+    # ------------------------------------------------------------ helpers
+    def _eng(self):
+        return self.session.engine()
+
+    @staticmethod
+    def _t(x):
+        return torch.as_tensor(np.asarray(x, np.float32))
+
+    def _q(self, arrays, target):
+        n = self.n
+        obs_n, act_n = list(arrays[:n]), list(arrays[n:2 * n])
+        i = self.agent_index
+        if self.local_q_func:                                          # maddpg.py:86-87
+            x = np.concatenate([np.asarray(obs_n[i], np.float32), np.asarray(act_n[i], np.float32)], 1)
+        else:                                                          # :85
+            x = np.concatenate([np.asarray(a, np.float32) for a in obs_n + act_n], 1)
+        return self._eng().q_values(i, self._t(x), target=target).cpu().numpy()
+
+    # ------------------------------------------------------------ surface
+    def action(self, obs):
+        """act(obs[None])[0] (maddpg.py:151-152): actor + Gumbel-softmax sample."""
+        return self._eng().act(self.agent_index, self._t(np.asarray(obs)[None])).cpu().numpy()[0]
+
+    def experience(self, obs, act, rew, new_obs, done, terminal):
+        self.replay_buffer.add(obs, act, rew, new_obs, float(done))    # :154-156
+
+    def preupdate(self):
+        self.replay_sample_index = None
+
+    def update(self, agents, t):
+        if len(self.replay_buffer) < self.max_replay_buffer_len:    # :162-163
+            return None
+        if not t % 100 == 0:                                          # :164-165
+            return None
+        for a in agents:
+            if a.session is not self.session:
+                raise RuntimeError("all agents of an update must share one session")
+        eng = self._eng()
+        self.session.flush()
+        idx = self.replay_buffer.make_index_device(self.args.batch_size)   # :167
+        self.replay_sample_index = idx
+        eng.update(self.agent_index, idx=idx)                           # :173-194
+        return UpdateStats(eng, self.agent_index)

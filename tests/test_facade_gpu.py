@@ -1,0 +1,145 @@
+"""Drop-in surface on the GPU: ReplayBuffer / MADDPGAgentTrainer / U.* / train.py,
+used exactly as the reference's own code uses them."""
+import argparse
+import hashlib
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from maddpg_amd.common import tf_util as U  # noqa: E402
+from maddpg_amd.envs import Discrete  # noqa: E402
+from maddpg_amd.trainer.maddpg import MADDPGAgentTrainer  # noqa: E402
+from maddpg_amd.trainer.replay_buffer import ReplayBuffer  # noqa: E402
+from oracle import mpe  # noqa: E402
+from oracle.pyrandom import MT19937  # noqa: E402
+from tests.helpers import golden_case  # noqa: E402
+
+
+def _digest(arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("name", ["small_s0", "wrap_s1", "spread_s12345"])
+def test_replay_buffer_facade_matches_reference(golden, name):
+    """replay_buffer.py used as the reference uses it: add, random.seed, make_index
+    per agent, sample_index of every agent's buffer (maddpg.py:167-178)."""
+    c = golden_case(golden, name)
+    data = c["data"]()
+    bufs = []
+    for (o, a, r, on, d) in data:
+        rb = ReplayBuffer(c["cap"])
+        for k in range(c["n_added"]):
+            rb.add(o[k], a[k], float(r[k]), on[k], float(d[k]))
+        bufs.append(rb)
+    assert len(bufs[0]) == min(c["cap"], c["n_added"])
+    random.seed(c["seed"])
+    n = len(c["dims"])
+    for i in range(n):
+        ix = bufs[i].make_index(c["B"])
+        assert ix == c["idx"][i].tolist()
+        arrs = []
+        for j in range(n):
+            o, a, _r, on, _d = bufs[j].sample_index(ix)
+            assert o.dtype == np.float64 and a.dtype == np.float32
+            arrs += [o, a, on]
+        own = bufs[i].sample_index(ix)
+        arrs += [own[2], own[4]]
+        assert _digest(arrs) == c["sha"][i]
+    np.testing.assert_array_equal(np.array(random.getstate()[1], np.uint32), c["state"])
+
+
+def test_trainer_facade_in_reference_loop(tmp_path):
+    """experiments/train.py:110-161 written against the drop-in classes, MPE on the host."""
+    args = argparse.Namespace(lr=1e-2, gamma=0.95, batch_size=64, num_units=64, max_episode_len=5)
+    sc = mpe.make("simple_spread")
+    rng = np.random.default_rng(0)
+    with U.single_threaded_session():
+        trainers = [MADDPGAgentTrainer(f"agent_{i}", None, [(18,)] * 3, [Discrete(5)] * 3, i, args)
+                    for i in range(3)]
+        U.initialize()
+        random.seed(5)
+        ref_rng = MT19937(5)
+        st = sc.reset(rng, 1)
+        obs_n = [o[0] for o in sc.observation(st)]
+        episode_step = train_step = 0
+        trained = 0
+        for _ in range(520):
+            action_n = [a.action(o) for a, o in zip(trainers, obs_n)]
+            for a in action_n:
+                assert a.shape == (5,) and a.dtype == np.float32 and abs(float(a.sum()) - 1) < 1e-5
+            st, new_obs_n, rew = sc.step(st, np.array(action_n)[None])
+            episode_step += 1
+            terminal = episode_step >= args.max_episode_len
+            for i, ag in enumerate(trainers):
+                ag.experience(obs_n[i], action_n[i], rew[0, i], new_obs_n[i][0], False, terminal)
+            obs_n = [o[0] for o in new_obs_n]
+            if terminal:
+                st = sc.reset(rng, 1)
+                obs_n = [o[0] for o in sc.observation(st)]
+                episode_step = 0
+            train_step += 1
+            for ag in trainers:
+                ag.preupdate()
+            for ag in trainers:
+                loss = ag.update(trainers, train_step)
+                gate = len(ag.replay_buffer) >= 320 and train_step % 100 == 0
+                if not gate:
+                    assert loss is None
+                    continue
+                trained += 1
+                want = ref_rng.make_index(len(ag.replay_buffer), 64)
+                np.testing.assert_array_equal(ag.replay_sample_index.cpu().numpy(), want)
+                assert len(loss) == 6 and all(np.isfinite(list(loss)))
+        assert trained == 3 * 5            # t = 100..500
+        assert random.getstate()[1] == ref_rng.state()
+        # p_debug / q_debug surfaces
+        ob = np.stack([obs_n[0]] * 7)
+        assert trainers[0].p_debug["target_act"](ob).shape == (7, 5)
+        assert trainers[0].p_debug["p_values"](ob).shape == (7, 5)
+        act = np.full((7, 5), 0.2, np.float32)
+        q = trainers[1].q_debug["target_q_values"](ob, ob, ob, act, act, act)
+        assert q.shape == (7,) and np.all(np.isfinite(q))
+        # save / restore round trip (tf_util.save_state / load_state)
+        eng = U.get_session().engine()
+        before = eng.get_params(2, "tgt_critic")["W2"].copy()
+        path = U.save_state(str(tmp_path) + "/")
+        eng.set_params(2, "tgt_critic", {k: v * 0 for k, v in eng.get_params(2, "tgt_critic").items()})
+        U.load_state(str(tmp_path) + "/")
+        np.testing.assert_array_equal(eng.get_params(2, "tgt_critic")["W2"], before)
+        assert os.path.exists(path)
+
+
+@pytest.mark.parametrize("scenario,extra", [
+    ("simple_spread", []),
+    ("simple_adversary", ["--num-adversaries", "1", "--adv-policy", "ddpg"]),
+    ("simple_tag", ["--num-adversaries", "3"]),
+    ("simple", []),
+])
+def test_train_cli_runs(tmp_path, capsys, scenario, extra):
+    from experiments.train import parse_args, train
+    a = parse_args(["--scenario", scenario, "--num-envs", "64", "--num-episodes", "300", "--save-rate", "100",
+                    "--batch-size", "64", "--max-episode-len", "5", "--save-dir", str(tmp_path) + "/",
+                    "--plots-dir", str(tmp_path) + "/", "--exp-name", "t"] + extra)
+    runner = train(a)
+    out = capsys.readouterr().out
+    assert "Starting iterations..." in out and "...Finished total of" in out
+    assert out.count("mean episode reward") >= 2
+    assert os.path.exists(str(tmp_path) + "/t_rewards.pkl")
+    assert runner.rounds > 0
+    # restore the saved model into a fresh run
+    a2 = parse_args(["--scenario", scenario, "--num-envs", "64", "--num-episodes", "10", "--restore",
+                     "--batch-size", "64", "--max-episode-len", "5", "--save-dir", str(tmp_path) + "/",
+                     "--plots-dir", str(tmp_path) + "/", "--exp-name", "t2"] + extra)
+    train(a2)
+    assert "Loading previous state..." in capsys.readouterr().out

@@ -1,0 +1,91 @@
+"""CPU tests of the host side: C-ABI exports, CLI surface, cadence, scenario tables."""
+import ctypes
+
+import pytest
+
+from maddpg_amd import _lib
+from maddpg_amd.envs import spec
+from maddpg_amd.runner import rounds_due
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 40
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(_lib.SIGNATURES) <= set(syms)
+    assert lib.mdp_abi_version() == 1
+
+
+def _cfg(**kw):
+    c = _lib.MdpConfig()
+    c.n_agents = 3
+    for i in range(3):
+        c.obs_dim[i] = 18
+    c.act_dim, c.num_units, c.batch_size, c.max_episode_len = 5, 64, 1024, 25
+    c.capacity, c.num_envs, c.scenario = 1000000, 1024, 2
+    c.lr, c.tau, c.grad_clip, c.actor_reg = 1e-2, 1e-2, 0.5, 1e-3
+    c.adam_b1, c.adam_b2, c.adam_eps, c.gamma = 0.9, 0.999, 1e-8, 0.95
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def test_arena_size_and_config_validation():
+    lib = _lib.load()
+    pt = ctypes.c_int64()
+    nb = lib.mdp_arena_bytes(ctypes.byref(_cfg()), ctypes.byref(pt))
+    # params: 3 x (actor 5701 + critic 8705) floats, each tensor padded to 4 floats
+    assert pt.value >= 3 * (5701 + 8705) and pt.value < 3 * (5701 + 8705) + 3 * 12 * 4
+    # replay 1e6 rows x 132 floats dominates
+    assert nb > 4 * 1_000_000 * 132
+    assert lib.mdp_arena_bytes(ctypes.byref(_cfg(num_units=96)), None) < 0      # H must be 64/128
+    assert lib.mdp_arena_bytes(ctypes.byref(_cfg(act_dim=4)), None) < 0
+    bad = _cfg()
+    bad.obs_dim[1] = 17                                                          # not simple_spread
+    assert lib.mdp_arena_bytes(ctypes.byref(bad), None) < 0
+    assert lib.mdp_arena_bytes(ctypes.byref(_cfg(scenario=0, num_envs=0)), None) > 0
+
+
+def test_cli_flags_mirror_reference_defaults():
+    from experiments.train import parse_args
+    a = parse_args([])
+    # experiments/train.py:14-36 of the reference
+    assert (a.scenario, a.max_episode_len, a.num_episodes, a.num_adversaries) == ("simple", 25, 60000, 0)
+    assert (a.good_policy, a.adv_policy, a.lr, a.gamma) == ("maddpg", "maddpg", 1e-2, 0.95)
+    assert (a.batch_size, a.num_units, a.exp_name, a.save_dir) == (1024, 64, None, "/tmp/policy/")
+    assert (a.save_rate, a.load_dir, a.restore, a.display, a.benchmark) == (1000, "", False, False, False)
+    assert (a.benchmark_iters, a.benchmark_dir, a.plots_dir) == (100000, "./benchmark_files/", "./learning_curves/")
+    assert a.num_envs == 1          # default = the reference's single env
+
+
+@pytest.mark.parametrize("t0,t1,want", [(0, 1, 0), (99, 100, 1), (100, 101, 0), (0, 1024, 10),
+                                        (1024, 2048, 10), (2010, 3100, 11), (0, 100, 1)])
+def test_update_cadence(t0, t1, want):
+    assert rounds_due(t0, t1) == want
+
+
+def test_cadence_e1_matches_reference_modulo():
+    # E=1: a round exactly at the steps where train_step % 100 == 0
+    hits = [t for t in range(1, 1001) if rounds_due(t - 1, t)]
+    assert hits == [t for t in range(1, 1001) if t % 100 == 0]
+
+
+def test_scenario_tables():
+    assert spec("simple").obs_dims == [4]
+    assert spec("simple_spread").obs_dims == [18, 18, 18]
+    assert spec("simple_adversary").obs_dims == [8, 10, 10]
+    assert spec("simple_tag").obs_dims == [16, 16, 16, 14]
+    assert spec("simple_tag", 6, 4).obs_dims == [22, 22, 22, 22, 20, 20]
+    with pytest.raises(ValueError):
+        spec("simple_crypto")
+
+
+def test_product_path_refuses_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from maddpg_amd.engine import Engine
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        Engine([4], batch_size=8, capacity=16)
