@@ -101,7 +101,7 @@ def test_trainer_facade_in_reference_loop(tmp_path):
                 want = ref_rng.make_index(len(ag.replay_buffer), 64)
                 np.testing.assert_array_equal(ag.replay_sample_index.cpu().numpy(), want)
                 assert len(loss) == 6 and all(np.isfinite(list(loss)))
-        assert trained == 3 * 5            # t = 100..500
+        assert trained == 3 * 2            # gate opens at 320 rows: t = 400, 500
         assert random.getstate()[1] == ref_rng.state()
         # p_debug / q_debug surfaces
         ob = np.stack([obs_n[0]] * 7)
