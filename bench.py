@@ -78,6 +78,20 @@ def roofline_for(kind, eng, ms_avg):
             "algorithmic_per_launch": by, "avg_launch_ms": ms_avg}
 
 
+def event_overhead_ms(stream, pairs=64):
+    """elapsed time of an EMPTY start/stop event pair on `stream` (what a bracketing
+    pair adds to every measured launch), median of `pairs` samples."""
+    evs = []
+    for _ in range(pairs):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        b.record(stream)
+        evs.append((a, b))
+    stream.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in evs)
+    return ts[len(ts) // 2]
+
+
 def load_traffic(kernel, config_key):
     """per-launch HBM bytes from a committed rocprofv3 PMC summary (profiles/pmc_*.json)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -175,7 +189,14 @@ def main():
     env_steps = args.num_envs * args.steps * world
     updates = rounds * r.n           # optimiser updates (each on world*B samples)
     value = env_steps / dt
-    roof = roofline_for(dominant, eng, ms_tot / max(launches, 1)) if launches else None
+    ev_ms = event_overhead_ms(eng.stream)
+    roof = None
+    if launches:
+        raw = ms_tot / launches
+        roof = roofline_for(dominant, eng, max(raw - ev_ms, 1e-6))
+        roof["avg_launch_ms_raw_events"] = raw
+        roof["event_pair_overhead_ms"] = ev_ms
+        roof["launches_timed"] = launches
     cfg_key = f"{args.scenario}_E{args.num_envs}_B{args.batch_size}_H{args.num_units}"
     if roof is not None:
         tr = load_traffic(roof["kernel"], cfg_key)

@@ -1,0 +1,84 @@
+"""Summarise rocprofv3 runs of bench.py into profiles/.
+
+    python tools/profile_summary.py --tag r01 --trace gpurun_out/prof_trace \
+        --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --bench gpurun_out/prof_bench.json
+
+Writes profiles/<tag>_kernel_stats.csv (the --kernel-trace --stats summary),
+profiles/<tag>_pmc.csv (per-kernel average FETCH_SIZE / WRITE_SIZE per launch)
+and updates profiles/pmc_traffic.json, which bench.py reads for the
+roofline's `traffic` field.  HBM bytes per launch follow
+MI355X_MICROARCH.md §HBM for gfx950: FETCH_SIZE (KiB) reports half of the
+bytes of wide coalesced reads -> x2; WRITE_SIZE (KiB) is exact for 16-B stores:
+    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+(other access widths are uncalibrated; the value is an estimate).
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    n = name.split("(")[0]
+    for pre in ("void ",):
+        if n.startswith(pre):
+            n = n[len(pre):]
+    return n.split("<")[0]
+
+
+def counters(d, cname):
+    agg = collections.defaultdict(list)
+    for f in os.listdir(d):
+        if f.endswith("counter_collection.csv"):
+            for r in csv.DictReader(open(os.path.join(d, f))):
+                if r["Counter_Name"] == cname:
+                    agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--bench")
+    ap.add_argument("--config-key", default=None)
+    a = ap.parse_args()
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = [f for f in os.listdir(a.trace) if f.endswith("kernel_stats.csv")][0]
+    shutil.copy(os.path.join(a.trace, stats), os.path.join(prof, f"{a.tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(os.path.join(a.trace, stats))))
+    avg_ns = {short(r["Name"]): float(r["AverageNs"]) for r in rows}
+    key = a.config_key
+    bench = None
+    if a.bench and os.path.exists(a.bench):
+        bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
+        if key is None:
+            cfg = bench["config"]
+            key = f"{cfg['scenario']}_E{cfg['num_envs_per_gpu']}_B{cfg['global_batch'] // bench['n_gpus']}_H64"
+        shutil.copy(a.bench, os.path.join(prof, f"{a.tag}_bench.json"))
+    out = {}
+    if a.fetch and a.write:
+        fe, wr = counters(a.fetch, "FETCH_SIZE"), counters(a.write, "WRITE_SIZE")
+        with open(os.path.join(prof, f"{a.tag}_pmc.csv"), "w") as fp:
+            fp.write("kernel,avg_ns,FETCH_SIZE_KiB,WRITE_SIZE_KiB,hbm_bytes_per_launch\n")
+            for k in sorted(set(fe) | set(wr)):
+                hb = (2 * fe.get(k, 0.0) + wr.get(k, 0.0)) * 1024
+                out[k] = {"fetch_kib": fe.get(k), "write_kib": wr.get(k), "hbm_bytes_per_launch": hb,
+                          "avg_ns": avg_ns.get(k)}
+                fp.write(f"{k},{avg_ns.get(k, '')},{fe.get(k, '')},{wr.get(k, '')},{hb:.0f}\n")
+        path = os.path.join(prof, "pmc_traffic.json")
+        allj = json.load(open(path)) if os.path.exists(path) else {}
+        allj[key] = dict(out, _source=f"{a.tag}_pmc.csv")
+        json.dump(allj, open(path, "w"), indent=1, sort_keys=True)
+    print(json.dumps({"tag": a.tag, "config_key": key, "avg_ns": avg_ns, "pmc": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
