@@ -153,8 +153,11 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev,
                const float* u_tgt_dev, const float* u_act_dev);
 /* gates of maddpg.py:162-165; returns 1 (skip) or 0 (train) */
 int mdp_update_gate(mdp_handle* h, int64_t t);
-/* update round: all agents in order (train.py:158-161), indices from the MT stream */
+/* update round: all agents in order (train.py:158-161), indices from the MT stream.
+ * Replayed from a captured hipGraph after the first round (see mdp_set_graphs). */
 int mdp_update_round(mdp_handle* h);
+/* enable (default) / disable hipGraph replay of mdp_update_round */
+int mdp_set_graphs(mdp_handle* h, int32_t on);
 /* phase entry points for data parallelism (grad -> all-reduce -> apply) */
 int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev);
 int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev);

@@ -258,6 +258,12 @@ struct mdp_handle {
   size_t ev_used[MDP_K_COUNT] = {};
   double prof_ms[MDP_K_COUNT] = {};
   int64_t prof_n[MDP_K_COUNT] = {};
+  // hipGraph of one update round (index draw + every agent's 6 kernels)
+  bool graphs = true;
+  bool capturing = false;
+  int eager_rounds = 0;
+  hipGraph_t round_graph = nullptr;
+  hipGraphExec_t round_exec = nullptr;
 };
 
 namespace {
@@ -285,7 +291,7 @@ struct ProfScope {
   int kind;
   hipEvent_t stop = nullptr;
   ProfScope(mdp_handle* hh, int k) : h(hh), kind(k) {
-    if (!h->prof_on[kind]) return;
+    if (!h->prof_on[kind] || h->capturing) return;
     auto& pool = h->ev[kind];
     size_t u = h->ev_used[kind];
     if (u + 2 > pool.size()) {
@@ -379,7 +385,13 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.slab_stat = h->stat_c;
   a.y_out = h->y;
   ProfScope p(h, MDP_K_CRITIC_GRAD);
-  HIPCHK(h, mdp_launch_critic_grad(a, h->cfg.num_units, lds_critic_bytes(h->L.topo), h->stream));
+  // as many target actors per pass as the LDS budget allows (all of them for S1-S4)
+  const int nact = h->L.topo.ag[agent].local_q ? 1 : h->cfg.n_agents;
+  int G = nact;
+  while (G > 1 && lds_critic_bytes(h->L.topo, G) > MDP_LDS_BUDGET) --G;
+  if (lds_critic_bytes(h->L.topo, G) > MDP_LDS_BUDGET) return fail(h, "critic step does not fit in LDS");
+  a.group = G;
+  HIPCHK(h, mdp_launch_critic_grad(a, h->cfg.num_units, lds_critic_bytes(h->L.topo, G), h->stream));
   return 0;
 }
 
@@ -588,6 +600,8 @@ int mdp_destroy(mdp_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (int k = 0; k < MDP_K_COUNT; ++k)
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
+  if (h->round_exec) (void)hipGraphExecDestroy(h->round_exec);
+  if (h->round_graph) (void)hipGraphDestroy(h->round_graph);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -829,12 +843,52 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
   return do_update(h, agent, idx, u_tgt_dev, u_act_dev);
 }
 
-int mdp_update_round(mdp_handle* h) {
+static int round_launches(mdp_handle* h) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   int rc = launch_make_index(h, n * B, h->index);
   if (rc) return rc;
   for (int i = 0; i < n; ++i)
     if ((rc = do_update(h, i, h->index + (int64_t)i * B, nullptr, nullptr))) return rc;
+  return 0;
+}
+
+static bool any_prof(const mdp_handle* h) {
+  for (int k = 0; k < MDP_K_COUNT; ++k)
+    if (h->prof_on[k]) return true;
+  return false;
+}
+
+// Every argument of the round's kernels is invariant (round-varying scalars --
+// replay length, MT19937 state, noise counter -- are read from the device
+// control block), so the round is captured once and replayed with one
+// hipGraphLaunch.  Per-kernel event profiling runs the eager path.
+int mdp_update_round(mdp_handle* h) {
+  if (h->len <= 0) return fail(h, "update round on an empty replay buffer");
+  if (!h->graphs || any_prof(h) || h->eager_rounds < 1) {
+    ++h->eager_rounds;  // the first round runs eagerly (one-time kernel attribute setup)
+    return round_launches(h);
+  }
+  if (!h->round_exec) {
+    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    h->capturing = true;
+    const int rc = round_launches(h);
+    h->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    if (e != hipSuccess) return fail(h, "hipStreamEndCapture", e);
+    h->round_graph = g;
+    HIPCHK(h, hipGraphInstantiate(&h->round_exec, g, nullptr, nullptr, 0));
+  }
+  HIPCHK(h, hipGraphLaunch(h->round_exec, h->stream));
+  return 0;
+}
+
+int mdp_set_graphs(mdp_handle* h, int32_t on) {
+  h->graphs = on != 0;
   return 0;
 }
 

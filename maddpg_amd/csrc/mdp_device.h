@@ -53,12 +53,12 @@ struct Philox {
 };
 
 // TF1 random_uniform float: mantissa from 23 random bits, value in [0, 1).
-__device__ inline float u01(uint32_t x) {
+__device__ __forceinline__ float u01(uint32_t x) {
   return __uint_as_float((x >> 9) | 0x3f800000u) - 1.0f;
 }
 
 // five uniforms for one (stream, counter, row) triple
-__device__ inline void uniforms5(uint64_t seed, uint32_t stream, uint32_t ctr, uint32_t row, float u[5]) {
+__device__ __forceinline__ void uniforms5(uint64_t seed, uint32_t stream, uint32_t ctr, uint32_t row, float u[5]) {
   uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   uint4 a = Philox::gen(make_uint4(row, ctr, stream, 0u), key);
   uint4 b = Philox::gen(make_uint4(row, ctr, stream, 1u), key);
@@ -66,19 +66,19 @@ __device__ inline void uniforms5(uint64_t seed, uint32_t stream, uint32_t ctr, u
 }
 
 // -------------------------------------------------------------- helpers
-__device__ inline float wave_sum(float v) {
+__device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ inline double wave_sum_d(double v) {
+__device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
 // workgroup-wide sum (all threads get the result); scratch >= MDP_NW doubles
-__device__ inline double block_sum_d(double v, double* scratch) {
+__device__ __forceinline__ double block_sum_d(double v, double* scratch) {
   v = wave_sum_d(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __syncthreads();
@@ -91,7 +91,7 @@ __device__ inline double block_sum_d(double v, double* scratch) {
 }
 
 // odd leading dimension so the 16 row-reads of one fragment land on distinct banks
-__host__ __device__ inline int lds_ld(int cols) { return (cols | 1); }
+__host__ __device__ __forceinline__ int lds_ld(int cols) { return (cols | 1); }
 
 // ------------------------------------------------------ MFMA layer tiles
 // Y[16][N] = act(X[16][K] @ W[K][N] + b)   X,Y in LDS; W,b global row-major [K][N]
@@ -99,40 +99,48 @@ __host__ __device__ inline int lds_ld(int cols) { return (cols | 1); }
 // B fragments of one 64-deep K chunk (16 MFMA k-steps) for one column: all 16
 // global loads are issued together so the chunk pays one L2 latency, not 16.
 #define MDP_KC 16
-__device__ inline void load_wchunk(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
+__device__ __forceinline__ void load_wchunk(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
                                    int K, int kq) {
+  const int kmax = K > 0 ? K - 1 : 0;
 #pragma unroll
   for (int s = 0; s < MDP_KC; ++s) {
     const int k = c0 + 4 * s + kq;
-    w[s] = k < K ? W[k * ldw + col] : 0.f;
+    const float v = W[min(k, kmax) * ldw + col];
+    w[s] = k < K ? v : 0.f;
   }
 }
 // same for a transposed operand: element (k, col) at W[col * ldw + k]
-__device__ inline void load_wchunk_t(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
+__device__ __forceinline__ void load_wchunk_t(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
                                      int K, int kq, bool colok) {
+  const int kmax = K > 0 ? K - 1 : 0;
 #pragma unroll
   for (int s = 0; s < MDP_KC; ++s) {
     const int k = c0 + 4 * s + kq;
-    w[s] = (k < K && colok) ? W[col * ldw + k] : 0.f;
+    const float v = W[col * ldw + min(k, kmax)];
+    w[s] = (k < K && colok) ? v : 0.f;
   }
 }
 // acc += A[r][c0 .. c0+63] . w  with A from LDS (row r = lane&15)
-__device__ inline f32x4 mfma_chunk(f32x4 acc, const float (&w)[MDP_KC], const float* A, int lda, int r, int c0,
+__device__ __forceinline__ f32x4 mfma_chunk(f32x4 acc, const float (&w)[MDP_KC], const float* A, int lda, int r, int c0,
                                    int K, int kq) {
+  const int kmax = K > 0 ? K - 1 : 0;
+  float x[MDP_KC];
 #pragma unroll
   for (int s = 0; s < MDP_KC; ++s) {
-    const int k0 = c0 + 4 * s;
-    if (k0 < K) {  // wave-uniform
-      const int k = k0 + kq;
-      const float a = k < K ? A[r * lda + k] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[s], acc, 0, 0, 0);
-    }
+    const int k = c0 + 4 * s + kq;
+    const float v = A[r * lda + min(k, kmax)];
+    x[s] = k < K ? v : 0.f;
+  }
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    if (c0 + 4 * s < K)  // wave-uniform
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
   }
   return acc;
 }
 
 template <bool RELU>
-__device__ inline void tile_fwd(const float* X, int ldx, int K, const float* __restrict__ W,
+__device__ __forceinline__ void tile_fwd(const float* X, int ldx, int K, const float* __restrict__ W,
                                 const float* __restrict__ b, int N, float* Y, int ldy) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kq = lane >> 4;
@@ -162,7 +170,7 @@ __device__ inline void tile_fwd(const float* X, int ldx, int K, const float* __r
 
 // dW[K][N] = X^T[K][16] @ dY[16][N], written to global (row-major, stride N).
 // Rows >= K are not written.
-__device__ inline void tile_wgrad(const float* X, int ldx, int K, const float* dY, int ldy, int N,
+__device__ __forceinline__ void tile_wgrad(const float* X, int ldx, int K, const float* dY, int ldy, int N,
                                   float* __restrict__ dW) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kq = lane >> 4;
@@ -188,7 +196,7 @@ __device__ inline void tile_wgrad(const float* X, int ldx, int K, const float* d
 
 // dX[16][K] = (dY[16][N] @ W^T) masked by (H > 0) where H is the layer input
 // (post-ReLU activations of the previous layer); K multiple of 16.
-__device__ inline void tile_dgrad_relu(const float* dY, int ldy, int N, const float* __restrict__ W, int K,
+__device__ __forceinline__ void tile_dgrad_relu(const float* dY, int ldy, int N, const float* __restrict__ W, int K,
                                        const float* Hin, int ldh, float* dX, int ldx) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, kq = lane >> 4;
@@ -216,7 +224,7 @@ __device__ inline void tile_dgrad_relu(const float* dY, int ldy, int N, const fl
 }
 
 // out[16][nout] = X[16][K] @ W[K][nout] + b  (small heads, VALU; 4 lanes per output)
-__device__ inline void tile_head(const float* X, int ldx, int K, const float* __restrict__ W,
+__device__ __forceinline__ void tile_head(const float* X, int ldx, int K, const float* __restrict__ W,
                                  const float* __restrict__ b, int nout, float* out, int ldo) {
   const int total = MDP_R * nout;
   for (int base = 0; base < total * 4; base += MDP_NT) {
@@ -237,7 +245,7 @@ __device__ inline void tile_head(const float* X, int ldx, int K, const float* __
 }
 
 // softmax(logits - log(-log(u))) on one row of 5 (distributions.py:264-266)
-__device__ inline void gumbel_softmax5(const float* logits, const float* u, float* a) {
+__device__ __forceinline__ void gumbel_softmax5(const float* logits, const float* u, float* a) {
   float z[MDP_ACT_DIM];
   float m = -INFINITY;
 #pragma unroll
@@ -253,6 +261,326 @@ __device__ inline void gumbel_softmax5(const float* logits, const float* u, floa
   }
 #pragma unroll
   for (int k = 0; k < MDP_ACT_DIM; ++k) a[k] = z[k] / s;
+}
+
+// ------------------------------------------------------ phase-parallel tiles
+// (k_critic_grad / k_actor_grad, 512-thread workgroups)  A "job" is one dense
+// layer Y[16][N] = act(X[16][K] @ W[K][N] + b) of one net; all jobs of a
+// phase are independent, their 16x16 output tiles are dealt over the waves
+// and each wave runs two tiles' MFMA chains interleaved (the 40-cycle
+// dependent latency of one chain is covered by the other's issue).  Every
+// weight fragment of both tiles is requested before the first MFMA, so a
+// phase pays one global-load latency instead of one per chunk.
+//
+// Job records live in LDS and hold OFFSETS, not pointers: X/Y index the
+// dynamic LDS segment, W/b index one of two global bases (online / target
+// parameters).  A pointer reloaded from LDS would be a generic address and
+// every access would become a FLAT load with a full vmcnt+lgkmcnt wait.
+struct FJob {
+  int xoff, ldx, K, woff, boff, yoff, ldy, wsel;
+};
+struct HJob {  // output head: out[16][nout] = X[16][K] @ W3[K][nout] + b3 (VALU)
+  int xoff, ldx, woff, boff, nout, ooff, ldo, wsel;
+};
+
+// unconditional (clamped, in-bounds) load + select: no branch per element
+__device__ __forceinline__ void load_wfrag(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
+                                           int K, int kq) {
+  const int kmax = K > 0 ? K - 1 : 0;
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    const int k = c0 + 4 * s + kq;
+    const float v = W[min(k, kmax) * ldw + col];
+    w[s] = k < K ? v : 0.f;
+  }
+}
+__device__ __forceinline__ void load_afrag(float (&a)[MDP_KC], const float* X, int ldx, int r, int c0, int K, int kq) {
+  const int kmax = K > 0 ? K - 1 : 0;
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    const int k = c0 + 4 * s + kq;
+    const float v = X[r * ldx + min(k, kmax)];
+    a[s] = k < K ? v : 0.f;
+  }
+}
+
+// acc_a += A_a . w_a and acc_b += A_b . w_b over one 64-deep chunk, alternating chains
+__device__ __forceinline__ void mfma_chunk2(f32x4& acc_a, const float (&xa)[MDP_KC], const float (&wa)[MDP_KC], int na,
+                                            f32x4& acc_b, const float (&xb)[MDP_KC], const float (&wb)[MDP_KC], int nb) {
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    if (s < na) acc_a = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], wa[s], acc_a, 0, 0, 0);
+    if (s < nb) acc_b = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], wb[s], acc_b, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ int ksteps(int K, int c0) {
+  const int left = K - c0;
+  return left <= 0 ? 0 : (left >= 4 * MDP_KC ? MDP_KC : (left + 3) >> 2);
+}
+
+// all jobs have N output columns (N multiple of 16); ReLU on every job
+__device__ __forceinline__ void fwd_phase(const FJob* jobs, int njobs, int N, float* lds, const float* __restrict__ P0,
+                                          const float* __restrict__ P1) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  const int ntl = N >> 4, total = njobs * ntl;
+  for (int t0 = wave; t0 < total; t0 += 2 * nw) {
+    const int t1 = t0 + nw;
+    const bool two = t1 < total;
+    const FJob ja = jobs[t0 / ntl];
+    const FJob jb = jobs[two ? t1 / ntl : t0 / ntl];
+    const int ca = (t0 % ntl) * 16 + r;
+    const int cb = two ? (t1 % ntl) * 16 + r : ca;
+    const int Kb = two ? jb.K : 0;
+    const float* Wa = (ja.wsel ? P1 : P0) + ja.woff;
+    const float* Wb = (jb.wsel ? P1 : P0) + jb.woff;
+    const float* Xa = lds + ja.xoff;
+    const float* Xb = lds + jb.xoff;
+    float wa0[MDP_KC], wa1[MDP_KC], wb0[MDP_KC], wb1[MDP_KC], xa[MDP_KC], xb[MDP_KC];
+    load_wfrag(wa0, Wa, N, ca, 0, ja.K, kq);
+    load_wfrag(wb0, Wb, N, cb, 0, Kb, kq);
+    const bool second = ja.K > 4 * MDP_KC || Kb > 4 * MDP_KC;
+    if (second) {
+      load_wfrag(wa1, Wa, N, ca, 4 * MDP_KC, ja.K, kq);
+      load_wfrag(wb1, Wb, N, cb, 4 * MDP_KC, Kb, kq);
+    }
+    const float biasa = (ja.wsel ? P1 : P0)[ja.boff + ca];
+    const float biasb = (jb.wsel ? P1 : P0)[jb.boff + cb];
+    f32x4 acc_a = {0.f, 0.f, 0.f, 0.f}, acc_b = {0.f, 0.f, 0.f, 0.f};
+    load_afrag(xa, Xa, ja.ldx, r, 0, ja.K, kq);
+    load_afrag(xb, Xb, jb.ldx, r, 0, Kb, kq);
+    mfma_chunk2(acc_a, xa, wa0, ksteps(ja.K, 0), acc_b, xb, wb0, ksteps(Kb, 0));
+    if (second) {
+      load_afrag(xa, Xa, ja.ldx, r, 4 * MDP_KC, ja.K, kq);
+      load_afrag(xb, Xb, jb.ldx, r, 4 * MDP_KC, Kb, kq);
+      mfma_chunk2(acc_a, xa, wa1, ksteps(ja.K, 4 * MDP_KC), acc_b, xb, wb1, ksteps(Kb, 4 * MDP_KC));
+      for (int c0 = 8 * MDP_KC; c0 < ja.K || c0 < Kb; c0 += 4 * MDP_KC) {   // K > 128: stream
+        load_wfrag(wa0, Wa, N, ca, c0, ja.K, kq);
+        load_wfrag(wb0, Wb, N, cb, c0, Kb, kq);
+        load_afrag(xa, Xa, ja.ldx, r, c0, ja.K, kq);
+        load_afrag(xb, Xb, jb.ldx, r, c0, Kb, kq);
+        mfma_chunk2(acc_a, xa, wa0, ksteps(ja.K, c0), acc_b, xb, wb0, ksteps(Kb, c0));
+      }
+    }
+    float* Ya = lds + ja.yoff;
+    float* Yb = lds + jb.yoff;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Ya[(kq * 4 + i) * ja.ldy + ca] = fmaxf(acc_a[i] + biasa, 0.f);
+      if (two) Yb[(kq * 4 + i) * jb.ldy + cb] = fmaxf(acc_b[i] + biasb, 0.f);
+    }
+  }
+}
+
+// heads of several nets, 4 lanes per output, nout <= 8
+__device__ __forceinline__ void head_phase(const HJob* jobs, int njobs, int K, float* lds, const float* __restrict__ P0,
+                                           const float* __restrict__ P1) {
+  int total = 0;
+  for (int j = 0; j < njobs; ++j) total += MDP_R * jobs[j].nout;
+  for (int base = 0; base < total * 4; base += blockDim.x) {
+    const int t = base + threadIdx.x;
+    const int o = t >> 2, q = t & 3;
+    float s = 0.f;
+    int jj = 0, oo = o;
+    const bool ok = o < total;
+    if (ok) {
+      while (oo >= MDP_R * jobs[jj].nout) {
+        oo -= MDP_R * jobs[jj].nout;
+        ++jj;
+      }
+    }
+    const HJob h = jobs[ok ? jj : 0];
+    const int row = ok ? oo / h.nout : 0, c = ok ? oo - row * h.nout : 0;
+    const float* X = lds + h.xoff;
+    const float* W = (h.wsel ? P1 : P0) + h.woff;
+    if (ok)
+      for (int k = q; k < K; k += 4) s = fmaf(X[row * h.ldx + k], W[k * h.nout + c], s);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (ok && q == 0) lds[h.ooff + row * h.ldo + c] = s + (h.wsel ? P1 : P0)[h.boff + c];
+  }
+}
+
+
+// ---------------------------------------------------------- wave-local nets
+// LDS ordering between lanes of ONE wave (no workgroup barrier)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One wave computes a whole layer Y[16][N] = act(X[16][K] @ W[K][N] + b) for
+// N = 16*NT: the NT column tiles' MFMA chains are interleaved (NT independent
+// accumulators), all weight fragments of a 64-deep chunk are loaded together.
+template <int NT, bool RELU>
+__device__ __forceinline__ void wave_layer(const float* X, int ldx, int K, const float* __restrict__ W,
+                                           const float* __restrict__ b, float* Y, int ldy) {
+  constexpr int N = NT * 16;
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < K; c0 += 4 * MDP_KC) {
+    float w[NT][MDP_KC], x[MDP_KC];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) load_wfrag(w[t], W, N, t * 16 + r, c0, K, kq);
+    load_afrag(x, X, ldx, r, c0, K, kq);
+    const int ns = ksteps(K, c0);
+#pragma unroll
+    for (int s = 0; s < MDP_KC; ++s) {
+      if (s < ns) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[t][s], acc[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float bias = b[t * 16 + r];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = acc[t][i] + bias;
+      if (RELU) v = fmaxf(v, 0.f);
+      Y[(kq * 4 + i) * ldy + t * 16 + r] = v;
+    }
+  }
+  wave_sync();
+}
+
+// one wave: out[16][nout] = X[16][K] @ W[K][nout] + b, nout <= 8 (4 lanes per output, passes of 16)
+__device__ __forceinline__ void wave_head(const float* X, int ldx, int K, const float* __restrict__ W,
+                                          const float* __restrict__ b, int nout, float* out, int ldo) {
+  const int lane = threadIdx.x & 63;
+  const int total = MDP_R * nout;
+  for (int base = 0; base < total; base += 16) {
+    const int o = base + (lane >> 2), q = lane & 3;
+    const bool ok = o < total;
+    const int row = ok ? o / nout : 0, c = ok ? o - row * nout : 0;
+    float s = 0.f;
+    for (int k = q; k < K; k += 4) s = fmaf(X[row * ldx + k], W[k * nout + c], s);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (ok && q == 0) out[row * ldo + c] = s + b[c];
+  }
+  wave_sync();
+}
+
+// one wave: dX[16][K] = (dY[16][N] @ W^T) masked by Hin > 0, W global [K][N], K = 16*NT
+template <int NT>
+__device__ __forceinline__ void wave_dgrad(const float* dY, int ldy, int N, const float* __restrict__ W,
+                                           const float* Hin, int ldh, float* dX, int ldx) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < N; c0 += 4 * MDP_KC) {
+    float w[NT][MDP_KC], x[MDP_KC];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) load_wchunk_t(w[t], W, N, t * 16 + r, c0, N, kq, true);
+    load_afrag(x, dY, ldy, r, c0, N, kq);
+#pragma unroll
+    for (int s = 0; s < MDP_KC; ++s) {
+      if (c0 + 4 * s < N) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[t][s], acc[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = kq * 4 + i, kk = t * 16 + r;
+      dX[row * ldx + kk] = Hin[row * ldh + kk] > 0.f ? acc[t][i] : 0.f;
+    }
+  }
+  wave_sync();
+}
+
+// dW tiles (M = K_feat rows of X^T, N = H) written to global, over the waves
+// starting at wave offset w0 (so the long dgrad chains can take other waves).
+__device__ __forceinline__ void wgrad_tiles(const float* X, int ldx, int K, const float* dY, int ldy, int N,
+                                   float* __restrict__ dW, int w0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  const int nmt = (K + 15) >> 4, nnt = N >> 4;
+  const int wv = (wave - w0 + nw) % nw;
+  for (int t = wv; t < nmt * nnt; t += nw) {
+    const int mt = t / nnt, nt = t - mt * nnt;
+    const int feat = mt * 16 + r;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r0 = 0; r0 < MDP_R; r0 += 4) {
+      const int row = r0 + kq;
+      const float a = feat < K ? X[row * ldx + feat] : 0.f;
+      const float g = dY[row * ldy + nt * 16 + r];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = mt * 16 + kq * 4 + i;
+      if (k < K) dW[k * N + nt * 16 + r] = acc[i];
+    }
+  }
+}
+
+// dX[16][K] = (dY[16][N] @ W^T) masked by Hin > 0, tiles over waves 0..K/16-1
+// (the caller keeps those waves free of other work); W global [K][N].
+__device__ __forceinline__ void dgrad_tiles(const float* dY, int ldy, int N, const float* __restrict__ W, int K,
+                                   const float* Hin, int ldh, float* dX, int ldx) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  for (int nt = wave; nt < (K >> 4); nt += nw) {
+    const int kk = nt * 16 + r;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < N; c0 += 4 * MDP_KC) {
+      float w[MDP_KC], x[MDP_KC];
+      load_wchunk_t(w, W, N, kk, c0, N, kq, true);
+      load_afrag(x, dY, ldy, r, c0, N, kq);
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s)
+        if (c0 + 4 * s < N) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = kq * 4 + i;
+      const float h = Hin[row * ldh + kk];
+      dX[row * ldx + kk] = h > 0.f ? acc[i] : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void gather_rows16(const float* __restrict__ replay, int stride, const int32_t* __restrict__ idx,
+                                     int r0, int nvalid, float* rowbuf, int ldr) {
+  const int v4 = stride >> 2;
+  for (int e = threadIdx.x; e < MDP_R * v4; e += blockDim.x) {
+    const int r = e / v4, c4 = e - r * v4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < nvalid) v = *reinterpret_cast<const float4*>(replay + (int64_t)idx[r0 + r] * stride + c4 * 4);
+    float* d = rowbuf + r * ldr + c4 * 4;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void copy_cols16(const float* src, int lds_src, int src_off, float* dst, int lds_dst, int dst_off,
+                                   int ncols) {
+  for (int e = threadIdx.x; e < MDP_R * ncols; e += blockDim.x) {
+    const int r = e / ncols, c = e - r * ncols;
+    dst[r * lds_dst + dst_off + c] = src[r * lds_src + src_off + c];
+  }
+}
+
+__device__ __forceinline__ void colsum16(const float* X, int ldx, int ncols, float* __restrict__ out) {
+  for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < MDP_R; ++r) s += X[r * ldx + c];
+    out[c] = s;
+  }
 }
 
 // Arena-relative LDS carving for the dynamic shared segment.

@@ -21,6 +21,7 @@ struct CriticArgs {
   int slab_stride;
   double* slab_stat;    // [nwg][8]
   double* y_out;        // [B]
+  int group;            // target actors run concurrently per pass (LDS budget)
 };
 
 struct ActorArgs {
@@ -135,14 +136,17 @@ struct EvalArgs {
 // ---- dynamic LDS sizes (must mirror the LdsCarve order in the kernels)
 inline int mdp_r4(int n) { return (n + 3) & ~3; }
 inline int mdp_ld(int c) { return c | 1; }
-inline int lds_critic_bytes(const Topo& t) {
-  const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), ldh = t.H + 1;
-  return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldc) + 6 * mdp_r4(R * ldh) + mdp_r4(R * 8) + 3 * mdp_r4(R) + 8);
+// k_critic_grad / k_actor_grad (mdp_grads.hip); FJob/HJob are 48-byte LDS job records
+inline int lds_critic_bytes(const Topo& t, int G) {
+  const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), S = R * (t.H + 1);
+  return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldc) + 2 * mdp_r4((G + 1) * S) + mdp_r4((G + 1) * R * 8) +
+              mdp_r4(R));
 }
 inline int lds_actor_bytes(const Topo& t) {
-  const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), ldh = t.H + 1;
-  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(R * ldh) + 4 * mdp_r4(R * 8) + mdp_r4(R) + 8);
+  const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), S = R * (t.H + 1);
+  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(S) + 5 * mdp_r4(R * 8));
 }
+#define MDP_LDS_BUDGET (160 * 1024)
 inline int lds_rollout_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), ldh = t.H + 1;
   return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8) + 2 * mdp_r4(R * 2 * MDP_MAX_ENT));

@@ -217,298 +217,6 @@ __device__ inline void mlp_fwd_tile(const float* X, int ldx, int K, const float*
 
 }  // namespace
 
-// One agent's critic step inputs and gradients (maddpg.py:180-188):
-// target actors of every agent on obs' (+ Gumbel), target critic, TD target
-// in fp64, critic forward, loss partials and per-workgroup critic gradients.
-template <int H>
-__global__ __launch_bounds__(MDP_NT) void k_critic_grad(CriticArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Topo& T = a.topo;
-  const ADesc& ag = T.ag[a.agent];
-  const int ldr = lds_ld(T.row_stride), ldc = lds_ld(T.cin_max), ldh = H + 1;
-  LdsCarve cv(lds);
-  float* rowbuf = cv.take(MDP_R * ldr);
-  float* xt = cv.take(MDP_R * ldc);
-  float* xl = cv.take(MDP_R * ldc);
-  float* h1 = cv.take(MDP_R * ldh);
-  float* h2 = cv.take(MDP_R * ldh);
-  float* h1c = cv.take(MDP_R * ldh);
-  float* h2c = cv.take(MDP_R * ldh);
-  float* d2 = cv.take(MDP_R * ldh);
-  float* d1 = cv.take(MDP_R * ldh);
-  float* lg = cv.take(MDP_R * 8);
-  float* qt = cv.take(MDP_R);
-  float* qv = cv.take(MDP_R);
-  float* dq = cv.take(MDP_R);
-  double* red = reinterpret_cast<double*>(cv.take(2 * MDP_NW));
-
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * MDP_R;
-  const int nvalid = min(MDP_R, a.B - r0);
-  const bool lq = ag.local_q != 0;
-  const uint32_t ctr = a.ctl->upd_ctr;
-  MDP_STAMP(0);
-
-  gather_tile(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-  __syncthreads();
-  MDP_STAMP(1);
-  __syncthreads();
-
-  // target critic input: [obs'_all | a~_all] (global) or [obs'_i | a~_i] (local)
-  if (lq) copy_cols(rowbuf, ldr, ag.nobs_off, xt, ldc, 0, ag.obs_dim);
-  else copy_cols(rowbuf, ldr, T.ag[0].nobs_off, xt, ldc, 0, T.sum_obs);
-
-  for (int j = 0; j < T.n; ++j) {
-    if (lq && j != a.agent) continue;   // a local critic only consumes a~_i
-    const ADesc& aj = T.ag[j];
-    mlp_fwd_tile<H>(rowbuf + aj.nobs_off, ldr, aj.obs_dim, a.target, aj.actor, h1, h2, ldh, lg, 8);
-    if (tid < MDP_R) {
-      float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
-      const int row = r0 + tid;
-      if (a.u_tgt) {
-        for (int k = 0; k < MDP_ACT_DIM; ++k)
-          u[k] = tid < nvalid ? a.u_tgt[((int64_t)j * a.B + row) * MDP_ACT_DIM + k] : 0.5f;
-      } else {
-        uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)row, u);
-      }
-      gumbel_softmax5(lg + tid * 8, u, act);
-      const int dst = lq ? ag.obs_dim : T.sum_obs + MDP_ACT_DIM * j;
-      for (int k = 0; k < MDP_ACT_DIM; ++k) xt[tid * ldc + dst + k] = act[k];
-    }
-    __syncthreads();
-    MDP_STAMP(2 + j);
-  }
-
-  MDP_STAMP(9);
-  // target critic -> Q'(o', a~)
-  mlp_fwd_tile<H>(xt, ldc, ag.cin, a.target, ag.critic, h1, h2, ldh, qt, 1);
-
-  MDP_STAMP(10);
-  // critic forward on (obs_n, act_n): the row's prefix (global) or [obs_i | act_i]
-  const float* X = rowbuf;
-  int ldX = ldr;
-  if (lq) {
-    copy_cols(rowbuf, ldr, ag.obs_off, xl, ldc, 0, ag.obs_dim);
-    copy_cols(rowbuf, ldr, ag.act_off, xl, ldc, ag.obs_dim, MDP_ACT_DIM);
-    __syncthreads();
-    X = xl;
-    ldX = ldc;
-  }
-  mlp_fwd_tile<H>(X, ldX, ag.cin, a.theta, ag.critic, h1c, h2c, ldh, qv, 1);
-
-  MDP_STAMP(11);
-  // TD target (fp64, maddpg.py:186), loss partials, dL/dq = 2(q - y)/B
-  double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;
-  if (tid < MDP_R) {
-    float g = 0.f;
-    if (tid < nvalid) {
-      const double rew = (double)rowbuf[tid * ldr + ag.rew_off];
-      const double done = (double)rowbuf[tid * ldr + ag.done_off];
-      const double qn = (double)qt[tid];
-      const double y64 = rew + a.gamma * (1.0 - done) * qn;
-      const float y = (float)y64;
-      const float diff = qv[tid] - y;
-      g = (2.0f * diff) * a.inv_b;
-      s_l = (double)diff * (double)diff;
-      s_y = y64;
-      s_r = rew;
-      s_q = qn;
-      a.y_out[r0 + tid] = y64;
-    }
-    dq[tid] = g;
-  }
-  s_l = block_sum_d(s_l, red);
-  s_y = block_sum_d(s_y, red);
-  s_r = block_sum_d(s_r, red);
-  s_q = block_sum_d(s_q, red);
-  if (tid == 0) {
-    double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
-    st[0] = s_l;
-    st[1] = s_y;
-    st[2] = s_r;
-    st[3] = s_q;
-  }
-  __syncthreads();
-
-  MDP_STAMP(12);
-  // backward through the critic (tf.gradients of q_loss w.r.t. q_func vars)
-  const NDesc& nd = ag.critic;
-  const float* W3 = a.theta + nd.t[4].off;
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
-  if (tid < H) {
-    float s = 0.f;
-    for (int r = 0; r < MDP_R; ++r) s = fmaf(h2c[r * ldh + tid], dq[r], s);
-    slab[nd.t[4].off + tid] = s;
-  }
-  if (tid == 0) {
-    float s = 0.f;
-    for (int r = 0; r < MDP_R; ++r) s += dq[r];
-    slab[nd.t[5].off] = s;
-  }
-  for (int e = tid; e < MDP_R * H; e += MDP_NT) {
-    const int r = e / H, h = e - r * H;
-    d2[r * ldh + h] = h2c[r * ldh + h] > 0.f ? dq[r] * W3[h] : 0.f;
-  }
-  __syncthreads();
-  tile_wgrad(h1c, ldh, H, d2, ldh, H, slab + nd.t[2].off);
-  colsum_store(d2, ldh, H, slab + nd.t[3].off);
-  tile_dgrad_relu(d2, ldh, H, a.theta + nd.t[2].off, H, h1c, ldh, d1, ldh);
-  __syncthreads();
-  MDP_STAMP(13);
-  tile_wgrad(X, ldX, ag.cin, d1, ldh, H, slab + nd.t[0].off);
-  colsum_store(d1, ldh, H, slab + nd.t[1].off);
-  __syncthreads();
-  MDP_STAMP(14);
-}
-
-// One agent's actor step gradients (maddpg.py:37-58): actor forward, fresh
-// Gumbel sample, critic (already updated) on the batch with a_i replaced,
-// backprop through the critic's a_i input slice, the softmax and the actor.
-template <int H>
-__global__ __launch_bounds__(MDP_NT) void k_actor_grad(ActorArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Topo& T = a.topo;
-  const ADesc& ag = T.ag[a.agent];
-  const int ldr = lds_ld(T.row_stride), ldc = lds_ld(T.cin_max), ldh = H + 1;
-  LdsCarve cv(lds);
-  float* rowbuf = cv.take(MDP_R * ldr);
-  float* x = cv.take(MDP_R * ldc);
-  float* h1a = cv.take(MDP_R * ldh);
-  float* h2a = cv.take(MDP_R * ldh);
-  float* h1c = cv.take(MDP_R * ldh);
-  float* h2c = cv.take(MDP_R * ldh);
-  float* d2 = cv.take(MDP_R * ldh);
-  float* d1 = cv.take(MDP_R * ldh);
-  float* lg = cv.take(MDP_R * 8);
-  float* av = cv.take(MDP_R * 8);
-  float* da = cv.take(MDP_R * 8);
-  float* dl = cv.take(MDP_R * 8);
-  float* qv = cv.take(MDP_R);
-  double* red = reinterpret_cast<double*>(cv.take(2 * MDP_NW));
-
-  const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * MDP_R;
-  const int nvalid = min(MDP_R, a.B - r0);
-  const bool lq = ag.local_q != 0;
-  const uint32_t ctr = a.ctl->upd_ctr;
-  const NDesc& na = ag.actor;
-  const NDesc& nc = ag.critic;
-
-  gather_tile(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-  __syncthreads();
-
-  // actor forward on obs_i -> logits p (maddpg.py:39)
-  mlp_fwd_tile<H>(rowbuf + ag.obs_off, ldr, ag.obs_dim, a.theta, na, h1a, h2a, ldh, lg, 8);
-  if (tid < MDP_R) {
-    float u[MDP_ACT_DIM];
-    const int row = r0 + tid;
-    if (a.u_act) {
-      for (int k = 0; k < MDP_ACT_DIM; ++k)
-        u[k] = tid < nvalid ? a.u_act[(int64_t)row * MDP_ACT_DIM + k] : 0.5f;
-    } else {
-      uniforms5(a.seed, (uint32_t)((a.agent << 8) | 0x80), ctr, (uint32_t)row, u);
-    }
-    gumbel_softmax5(lg + tid * 8, u, av + tid * 8);
-  }
-  // critic input with act_input_n[i] = gumbel sample (maddpg.py:48-52)
-  if (lq) {
-    copy_cols(rowbuf, ldr, ag.obs_off, x, ldc, 0, ag.obs_dim);
-  } else {
-    copy_cols(rowbuf, ldr, 0, x, ldc, 0, ag.cin);
-  }
-  __syncthreads();
-  if (tid < MDP_R) {
-    for (int k = 0; k < MDP_ACT_DIM; ++k) x[tid * ldc + ag.a_in_off + k] = av[tid * 8 + k];
-  }
-  __syncthreads();
-  mlp_fwd_tile<H>(x, ldc, ag.cin, a.theta, nc, h1c, h2c, ldh, qv, 1);
-
-  // loss partials: -mean(q) + reg * mean(p^2)
-  double s_q = 0.0, s_p = 0.0;
-  if (tid < nvalid) {
-    s_q = (double)qv[tid];
-    for (int k = 0; k < MDP_ACT_DIM; ++k) {
-      const double p = (double)lg[tid * 8 + k];
-      s_p += p * p;
-    }
-  }
-  s_q = block_sum_d(s_q, red);
-  s_p = block_sum_d(s_p, red);
-  if (tid == 0) {
-    double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
-    st[0] = s_q;
-    st[1] = s_p;
-  }
-
-  // dL/dq = -1/B ; back through critic layers 3, 2 to h1
-  const float* W3c = a.theta + nc.t[4].off;
-  for (int e = tid; e < MDP_R * H; e += MDP_NT) {
-    const int r = e / H, h = e - r * H;
-    d2[r * ldh + h] = (r < nvalid && h2c[r * ldh + h] > 0.f) ? a.neg_inv_b * W3c[h] : 0.f;
-  }
-  __syncthreads();
-  tile_dgrad_relu(d2, ldh, H, a.theta + nc.t[2].off, H, h1c, ldh, d1, ldh);
-  __syncthreads();
-  // da[r][k] = sum_h d1[r][h] * W1c[a_in_off + k][h]   (only the a_i input columns)
-  {
-    const float* W1c = a.theta + nc.t[0].off + (int64_t)ag.a_in_off * H;
-    for (int base = 0; base < MDP_R * MDP_ACT_DIM * 4; base += MDP_NT) {
-      const int t = base + tid;
-      const int o = t >> 2, q = t & 3;
-      float s = 0.f;
-      if (o < MDP_R * MDP_ACT_DIM) {
-        const int r = o / MDP_ACT_DIM, k = o - r * MDP_ACT_DIM;
-        for (int h = q; h < H; h += 4) s = fmaf(d1[r * ldh + h], W1c[k * H + h], s);
-      }
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      if (o < MDP_R * MDP_ACT_DIM && q == 0) {
-        const int r = o / MDP_ACT_DIM, k = o - r * MDP_ACT_DIM;
-        da[r * 8 + k] = s;
-      }
-    }
-  }
-  __syncthreads();
-  // softmax backward + regulariser: dlogits = (da - sum(a*da)) * a + reg*2*p/(B*A)
-  if (tid < MDP_R) {
-    float dot = 0.f;
-    for (int k = 0; k < MDP_ACT_DIM; ++k) dot += da[tid * 8 + k] * av[tid * 8 + k];
-    for (int k = 0; k < MDP_ACT_DIM; ++k) {
-      const float g = (da[tid * 8 + k] - dot) * av[tid * 8 + k] + lg[tid * 8 + k] * a.reg_scale;
-      dl[tid * 8 + k] = tid < nvalid ? g : 0.f;
-    }
-  }
-  __syncthreads();
-
-  // actor backward
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
-  const float* W3a = a.theta + na.t[4].off;
-  for (int e = tid; e < H * MDP_ACT_DIM; e += MDP_NT) {
-    const int h = e / MDP_ACT_DIM, k = e - h * MDP_ACT_DIM;
-    float s = 0.f;
-    for (int r = 0; r < MDP_R; ++r) s = fmaf(h2a[r * ldh + h], dl[r * 8 + k], s);
-    slab[na.t[4].off + e] = s;
-  }
-  if (tid < MDP_ACT_DIM) {
-    float s = 0.f;
-    for (int r = 0; r < MDP_R; ++r) s += dl[r * 8 + tid];
-    slab[na.t[5].off + tid] = s;
-  }
-  for (int e = tid; e < MDP_R * H; e += MDP_NT) {
-    const int r = e / H, h = e - r * H;
-    float s = 0.f;
-    for (int k = 0; k < MDP_ACT_DIM; ++k) s = fmaf(dl[r * 8 + k], W3a[h * MDP_ACT_DIM + k], s);
-    d2[r * ldh + h] = h2a[r * ldh + h] > 0.f ? s : 0.f;
-  }
-  __syncthreads();
-  tile_wgrad(h1a, ldh, H, d2, ldh, H, slab + na.t[2].off);
-  colsum_store(d2, ldh, H, slab + na.t[3].off);
-  tile_dgrad_relu(d2, ldh, H, a.theta + na.t[2].off, H, h1a, ldh, d1, ldh);
-  __syncthreads();
-  tile_wgrad(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1, ldh, H, slab + na.t[0].off);
-  colsum_store(d1, ldh, H, slab + na.t[1].off);
-}
-
 // ================================================================ apply
 namespace {
 // true in every thread of the last workgroup to arrive (no static LDS: keeps
@@ -541,19 +249,27 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs a) {
     a.beta[1] = p2 * a.b2;
     if (a.bump_ctr) a.ctl->upd_ctr += 1u;
   }
-  if (e >= a.size) return;
-  const float* p = a.slab + e;
+  // 8 lanes per element: lane q sums partials w = q, q+8, ... (all loads in
+  // flight at once), then a fixed xor-tree over the 8 lanes -> deterministic
+  const int64_t el = e >> 3;
+  const int q = (int)(e & 7);
   float s = 0.f;
-  int w = 0;
-  for (; w + 8 <= a.nwg; w += 8) {
+  if (el < a.size) {
+    const float* p = a.slab + el;
     float v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = p[(int64_t)(w + q) * a.slab_stride];
+    for (int k = 0; k < 8; ++k) {
+      const int w = q + 8 * k;
+      v[k] = w < a.nwg ? p[(int64_t)w * a.slab_stride] : 0.f;
+    }
+    for (int w = q + 64; w < a.nwg; w += 8) s += p[(int64_t)w * a.slab_stride];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s += v[q];
+    for (int k = 0; k < 8; ++k) s += v[k];
   }
-  for (; w < a.nwg; ++w) s += p[(int64_t)w * a.slab_stride];
-  a.grad[a.off + e] = s;
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (el < a.size && q == 0) a.grad[a.off + el] = s;
 }
 
 // Workgroup (tensor t, chunk c) of `net`: per-tensor clip_by_norm (norm of the
@@ -572,10 +288,18 @@ __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
     const TDesc td = a.net.t[t];
     const int n = td.rows * td.cols;
     const float* g = a.grad + td.off;
+    // all of this thread's loads are issued before the first is consumed
+    // (a rolled loop would pay one memory round trip per element)
     double ss = 0.0;
-    for (int e = tid; e < n; e += blockDim.x) {
-      const float v = g[e] * a.scale;
-      ss += (double)v * (double)v;
+    for (int e0 = tid; e0 < n; e0 += 8 * blockDim.x) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int e = e0 + q * blockDim.x;
+        v[q] = e < n ? g[min(e, n - 1)] * a.scale : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss += (double)v[q] * (double)v[q];
     }
     ss = block_sum_d(ss, red);
     const float norm = (float)sqrt(ss);
@@ -611,41 +335,38 @@ __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
     }
   } else if (a.stats_mode) {
     // stats workgroup (maddpg.py:196): critic fills 0,2,3,4,5; actor fills 1
-    if (a.stats_mode == 1) {
-      double sl = 0.0, sy = 0.0, sr = 0.0, sq = 0.0;
-      if (tid == 0) {
-        for (int w = 0; w < a.nwg; ++w) {
-          const double* st = a.slab_stat + (int64_t)w * 8;
-          sl += st[0];
-          sy += st[1];
-          sr += st[2];
-          sq += st[3];
+    // one wave, lane-strided partial sums + fixed xor trees (deterministic, no barriers)
+    if (tid < 64) {
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+      for (int w = tid; w < a.nwg; w += 64) {
+        const double* st = a.slab_stat + (int64_t)w * 8;
+        s0 += st[0];
+        s1 += st[1];
+        s2 += st[2];
+        s3 += st[3];
+      }
+      s0 = wave_sum_d(s0);
+      s1 = wave_sum_d(s1);
+      if (a.stats_mode == 1) {
+        s2 = wave_sum_d(s2);
+        s3 = wave_sum_d(s3);
+        const double mean_y = s1 / a.B;
+        double dv = 0.0;
+        for (int i = tid; i < a.B; i += 64) {
+          const double d = a.y[i] - mean_y;
+          dv += d * d;
         }
-        red[0] = sy / a.B;
+        dv = wave_sum_d(dv);
+        if (tid == 0) {
+          a.stats_out[0] = s0 / a.B;
+          a.stats_out[2] = mean_y;
+          a.stats_out[3] = s2 / a.B;
+          a.stats_out[4] = s3 / a.B;
+          a.stats_out[5] = sqrt(dv / a.B);
+        }
+      } else if (tid == 0) {
+        a.stats_out[1] = -s0 / a.B + (double)a.reg * (s1 / ((double)a.B * MDP_ACT_DIM));
       }
-      __syncthreads();
-      const double mean_y = red[0];
-      double dv = 0.0;
-      for (int i = tid; i < a.B; i += blockDim.x) {
-        const double d = a.y[i] - mean_y;
-        dv += d * d;
-      }
-      __syncthreads();
-      dv = block_sum_d(dv, red);
-      if (tid == 0) {
-        a.stats_out[0] = sl / a.B;
-        a.stats_out[2] = mean_y;
-        a.stats_out[3] = sr / a.B;
-        a.stats_out[4] = sq / a.B;
-        a.stats_out[5] = sqrt(dv / a.B);
-      }
-    } else if (tid == 0) {
-      double sq = 0.0, sp = 0.0;
-      for (int w = 0; w < a.nwg; ++w) {
-        sq += a.slab_stat[(int64_t)w * 8 + 0];
-        sp += a.slab_stat[(int64_t)w * 8 + 1];
-      }
-      a.stats_out[1] = -sq / a.B + (double)a.reg * (sp / ((double)a.B * MDP_ACT_DIM));
     }
   }
 }
@@ -1111,20 +832,6 @@ __global__ __launch_bounds__(MDP_NT) void k_mlp_eval(EvalArgs a) {
   } while (0)
 
 template <int H>
-static hipError_t launch_critic_grad_t(const CriticArgs& a, int lds_bytes, hipStream_t s) {
-  const int grid = (a.B + MDP_R - 1) / MDP_R;
-  hipLaunchKernelGGL(k_critic_grad<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
-  MDP_CHECK_LAUNCH();
-  return hipSuccess;
-}
-template <int H>
-static hipError_t launch_actor_grad_t(const ActorArgs& a, int lds_bytes, hipStream_t s) {
-  const int grid = (a.B + MDP_R - 1) / MDP_R;
-  hipLaunchKernelGGL(k_actor_grad<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
-  MDP_CHECK_LAUNCH();
-  return hipSuccess;
-}
-template <int H>
 static hipError_t launch_rollout_t(const RolloutArgs& a, int lds_bytes, hipStream_t s) {
   const int grid = (a.E + MDP_R - 1) / MDP_R;
   hipLaunchKernelGGL(k_rollout<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
@@ -1142,8 +849,6 @@ static hipError_t launch_eval_t(const EvalArgs& a, int lds_bytes, hipStream_t s)
 static int set_lds_limit_done = 0;
 template <int H>
 static void raise_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_critic_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-  (void)hipFuncSetAttribute((const void*)k_actor_grad<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
   (void)hipFuncSetAttribute((const void*)k_rollout<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
   (void)hipFuncSetAttribute((const void*)k_mlp_eval<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
 }
@@ -1156,14 +861,6 @@ static void ensure_lds_limits() {
   }
 }
 
-hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s) {
-  ensure_lds_limits();
-  return H == 64 ? launch_critic_grad_t<64>(a, lds_bytes, s) : launch_critic_grad_t<128>(a, lds_bytes, s);
-}
-hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s) {
-  ensure_lds_limits();
-  return H == 64 ? launch_actor_grad_t<64>(a, lds_bytes, s) : launch_actor_grad_t<128>(a, lds_bytes, s);
-}
 hipError_t mdp_launch_rollout(const RolloutArgs& a, int H, int lds_bytes, hipStream_t s) {
   ensure_lds_limits();
   return H == 64 ? launch_rollout_t<64>(a, lds_bytes, s) : launch_rollout_t<128>(a, lds_bytes, s);
@@ -1179,7 +876,7 @@ hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s) {
   return hipSuccess;
 }
 hipError_t mdp_launch_reduce(const ReduceArgs& a, hipStream_t s) {
-  const int grid = (int)((a.size + 255) / 256);
+  const int grid = (int)((a.size * 8 + 255) / 256);
   hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, s, a);
   MDP_CHECK_LAUNCH();
   return hipSuccess;
@@ -1241,9 +938,3 @@ hipError_t mdp_launch_set_ring(Ctl* ctl, int64_t len, int64_t next, hipStream_t 
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
-
-#ifdef MDP_STAMPS
-extern "C" int mdp_debug_stamps(unsigned long long* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
-}
-#endif

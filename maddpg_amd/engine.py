@@ -332,6 +332,10 @@ class Engine:
     def update_round(self):
         self._c("mdp_update_round")
 
+    def set_graphs(self, on=True):
+        """hipGraph replay of update_round (default on; per-kernel profiling runs eager)."""
+        self._c("mdp_set_graphs", 1 if on else 0)
+
     def critic_grad(self, agent, idx, u_tgt=None):
         self._c("mdp_critic_grad", agent, self._ptr(idx), self._ptr(u_tgt))
 

@@ -22,18 +22,18 @@ eng.init_params(0)
 eng.seed_py_random(0)
 lib = _lib.load()
 lib.mdp_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-names = {0: "start", 1: "gather", 2: "tgt actor 0", 3: "tgt actor 1", 4: "tgt actor 2", 9: "-", 10: "tgt critic",
-         11: "critic fwd", 12: "TD+stats", 13: "dW3,dW2,dh1", 14: "dW1,db1"}
+names = {0: "start", 1: "gather+copies", 2: "tgt actors+critic fwd", 3: "tgt critic", 4: "TD,stats,dW3,d2",
+         5: "dh1,dW2,dW1"}
 for it in range(5):
     eng.update_round()
     eng.synchronize()
 buf = (ctypes.c_ulonglong * 64)()
 lib.mdp_debug_stamps(buf, 64)
-st = np.array(buf[:15], dtype=np.int64)
+st = np.array(buf[:6], dtype=np.int64)
 prev = st[0]
-for i in range(1, 15):
-    if st[i] == 0 or i in (5, 6, 7, 8):
+for i in range(1, 6):
+    if st[i] == 0:
         continue
     print(f"{names.get(i, i):>14s}: {(st[i] - prev) * 10 / 1000:7.2f} us")
     prev = st[i]
-print(f"{'total':>14s}: {(st[14] - st[0]) * 10 / 1000:7.2f} us")
+print(f"{'total':>14s}: {(st[5] - st[0]) * 10 / 1000:7.2f} us")
