@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -262,6 +263,9 @@ struct mdp_handle {
   bool graphs = true;
   bool capturing = false;
   int eager_rounds = 0;
+  // MDP_GENERAL_GRADS=1 in the environment at create: always use the general
+  // grad kernels (mdp_grads.hip) -- lets tests compare both paths
+  bool general_grads = false;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
 };
@@ -385,6 +389,10 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.slab_stat = h->stat_c;
   a.y_out = h->y;
   ProfScope p(h, MDP_K_CRITIC_GRAD);
+  if (!h->general_grads && grads_r_ok(h->L.topo, agent)) {
+    HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
+    return 0;
+  }
   // as many target actors per pass as the LDS budget allows (all of them for S1-S4)
   const int nact = h->L.topo.ag[agent].local_q ? 1 : h->cfg.n_agents;
   int G = nact;
@@ -412,6 +420,10 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
   a.slab_stride = h->L.slab_a;
   a.slab_stat = h->stat_a;
   ProfScope p(h, MDP_K_ACTOR_GRAD);
+  if (!h->general_grads && grads_r_ok(h->L.topo, agent)) {
+    HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
+    return 0;
+  }
   HIPCHK(h, mdp_launch_actor_grad(a, h->cfg.num_units, lds_actor_bytes(h->L.topo), h->stream));
   return 0;
 }
@@ -525,6 +537,10 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     return -1;
   }
   h->cfg = *cfg;
+  {
+    const char* g = getenv("MDP_GENERAL_GRADS");
+    h->general_grads = g && g[0] == '1';
+  }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
     *out = h;

@@ -594,3 +594,183 @@ struct LdsCarve {
     return p;
   }
 };
+
+// ------------------------------------------- register-resident layers (H = 64)
+// Used by the fast gradient kernels (mdp_grads_r.hip).  Every weight a wave
+// needs is loaded into its registers at kernel start -- one memory round trip
+// for the whole kernel, overlapped with the replay gather -- instead of one
+// per layer.  Forward layers keep all four 16-column tiles in one wave with a
+// PERMUTED column map: tile t, lane (r = lane & 15, kq = lane >> 4) produces
+// column 4r + t, so a lane's B fragments at one k-step are 4 consecutive
+// floats of a weight row (one 16-B load).  Contraction index k = 4s + kq.
+#define MDP_RH 64   // hidden width of the register-resident path
+#define MDP_RLH 68  // LDS row stride of forward activations (4r + kq: 64 distinct banks)
+#define MDP_RLD 65  // LDS row stride of backward deltas (r + 16 kq + s: 64 distinct banks)
+
+__device__ __forceinline__ f32x4 ld4(const float* __restrict__ p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// w[s] = W[4s+kq][4r .. 4r+3] of W[K][64]; rows >= K or inside [mlo, mhi) read as zero
+template <int KS>
+__device__ __forceinline__ void rf_load(f32x4 (&w)[KS], const float* __restrict__ W, int K, int mlo, int mhi) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    w[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (4 * s < K) {
+      const int k = 4 * s + kq;
+      const f32x4 v = ld4(W + min(k, K - 1) * MDP_RH + 4 * r);
+      const bool z = k >= K || (k >= mlo && k < mhi);
+      w[s] = f32x4{z ? 0.f : v[0], z ? 0.f : v[1], z ? 0.f : v[2], z ? 0.f : v[3]};
+    }
+  }
+}
+
+// acc[t] += X[16][K] @ W (the fragments of rf_load); X in LDS
+template <int KS>
+__device__ __forceinline__ void rf_acc(f32x4 (&acc)[4], const float* X, int ldx, int K, const f32x4 (&w)[KS]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const float* xr = X + r * ldx;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (4 * s < K) {
+      const float x = xr[min(4 * s + kq, K - 1)];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x, w[s][t], acc[t], 0, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void rf_zero(f32x4 (&acc)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// Y[16][64] = act(acc + b), b = bias[4r .. 4r+3]; Y row stride a multiple of 4 (16-B stores)
+template <bool RELU>
+__device__ __forceinline__ void rf_store(const f32x4 (&acc)[4], f32x4 b, float* Y, int ldy) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f32x4 v;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = RELU ? fmaxf(acc[t][i] + b[t], 0.f) : acc[t][i] + b[t];
+    *reinterpret_cast<f32x4*>(Y + (kq * 4 + i) * ldy + 4 * r) = v;
+  }
+}
+
+// output head with nout <= 16 columns on one MFMA tile (column r), K = 64
+__device__ __forceinline__ void rh_load(float (&w)[16], const float* __restrict__ W, int nout) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int c = min(r, nout - 1);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const float v = W[(4 * s + kq) * nout + c];
+    w[s] = r < nout ? v : 0.f;
+  }
+}
+__device__ __forceinline__ f32x4 rh_acc(const float* X, int ldx, const float (&w)[16]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(X[r * ldx + 4 * s + kq], w[s], acc, 0, 0, 0);
+  return acc;
+}
+
+// scalar head (nout = 1) on the VALU: lane (row = lane >> 2, q = lane & 3), w[j] = W3[4j + q]
+__device__ __forceinline__ void rq_load(float (&w)[16], const float* __restrict__ W) {
+  const int q = threadIdx.x & 3;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = W[4 * j + q];
+}
+// returns sum_k X[row][k] W3[k] in all 4 lanes of the row
+__device__ __forceinline__ float rq_head(const float* X, int ldx, const float (&w)[16]) {
+  const int lane = threadIdx.x & 63, row = lane >> 2, q = lane & 3;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s = fmaf(X[row * ldx + 4 * j + q], w[j], s);
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  return s;
+}
+
+// one 16-column tile per wave (column col = 16 tt + r of W[K][ldw]), k = 4s + kq
+template <int KS>
+__device__ __forceinline__ void rt_load(float (&w)[KS], const float* __restrict__ W, int ldw, int col, int K) {
+  const int kq = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    w[s] = 0.f;
+    if (4 * s < K) {
+      const int k = 4 * s + kq;
+      const float v = W[min(k, K - 1) * ldw + col];
+      w[s] = k < K ? v : 0.f;
+    }
+  }
+}
+template <int KS>
+__device__ __forceinline__ void rt_acc(f32x4& acc, const float* X, int ldx, int K, const float (&w)[KS]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const float* xr = X + r * ldx;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[min(4 * s + kq, K - 1)], w[s], acc, 0, 0, 0);
+}
+
+// transposed tile for dX = dY @ W^T (W[K][64] row-major): output column kk = W row,
+// contraction n = 16 kq + s, so a lane's 16 fragments are one contiguous 64-B run
+// of row kk: w[m] = W[kk][16 kq + 4m .. +3]; ok = false zeroes the fragment
+__device__ __forceinline__ void rdg_load(f32x4 (&w)[4], const float* __restrict__ W, int kk, bool ok) {
+  const int kq = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const f32x4 v = ld4(W + kk * MDP_RH + 16 * kq + 4 * m);
+    w[m] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+__device__ __forceinline__ f32x4 rdg_acc(const float* dY, int ldy, const f32x4 (&w)[4]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const float* yr = dY + r * ldy + 16 * kq;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(yr[s], w[s >> 2][s & 3], acc, 0, 0, 0);
+  return acc;
+}
+
+// ------------------------------------------------ shared by the grad kernels
+// lanes 0..15 hold one value each; returns the sum in every lane (fixed order)
+__device__ __forceinline__ double sum16(double v) {
+  const int lane = threadIdx.x & 63;
+  v = lane < MDP_R ? v : 0.0;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// weight-gradient tiles over waves [w0, w0 + wn)
+__device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, const float* dY, int ldy, int N,
+                                            float* __restrict__ dW, int w0, int wn) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave < w0 || wave >= w0 + wn) return;
+  const int r = lane & 15, kq = lane >> 4;
+  const int nmt = (K + 15) >> 4, nnt = N >> 4;
+  for (int t = wave - w0; t < nmt * nnt; t += wn) {
+    const int mt = t / nnt, nt = t - mt * nnt;
+    const int feat = mt * 16 + r;
+    const int fc = min(feat, K - 1);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r0 = 0; r0 < MDP_R; r0 += 4) {
+      const int row = r0 + kq;
+      const float xv = X[row * ldx + fc];
+      const float a = feat < K ? xv : 0.f;
+      const float g = dY[row * ldy + nt * 16 + r];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = mt * 16 + kq * 4 + i;
+      if (k < K) dW[k * N + nt * 16 + r] = acc[i];
+    }
+  }
+}
+

@@ -24,46 +24,6 @@
 #include "mdp_device.h"
 #include "mdp_kernels.h"
 
-namespace {
-
-// lanes 0..15 hold one value each; returns the sum in every lane (fixed order)
-__device__ __forceinline__ double sum16(double v) {
-  const int lane = threadIdx.x & 63;
-  v = lane < MDP_R ? v : 0.0;
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// weight-gradient tiles over waves [w0, w0 + wn)
-__device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, const float* dY, int ldy, int N,
-                                            float* __restrict__ dW, int w0, int wn) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (wave < w0 || wave >= w0 + wn) return;
-  const int r = lane & 15, kq = lane >> 4;
-  const int nmt = (K + 15) >> 4, nnt = N >> 4;
-  for (int t = wave - w0; t < nmt * nnt; t += wn) {
-    const int mt = t / nnt, nt = t - mt * nnt;
-    const int feat = mt * 16 + r;
-    const int fc = min(feat, K - 1);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r0 = 0; r0 < MDP_R; r0 += 4) {
-      const int row = r0 + kq;
-      const float xv = X[row * ldx + fc];
-      const float a = feat < K ? xv : 0.f;
-      const float g = dY[row * ldy + nt * 16 + r];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = mt * 16 + kq * 4 + i;
-      if (k < K) dW[k * N + nt * 16 + r] = acc[i];
-    }
-  }
-}
-
-}  // namespace
 
 template <int H>
 __global__ __launch_bounds__(512) void k_critic_grad(CriticArgs a) {

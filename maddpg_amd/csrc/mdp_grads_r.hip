@@ -1,0 +1,523 @@
+// mdp_grads_r.hip -- fast critic-step / actor-step gradient kernels for H = 64.
+//
+// Same contract and outputs as k_critic_grad / k_actor_grad (mdp_grads.hip;
+// per-workgroup partial gradients of 16 batch rows, reduced by k_reduce), for
+// the topologies grads_r_ok() admits (every S1-S3 configuration at H = 64).
+//
+// What is different: every wave loads ALL the weights it will use into its
+// registers at kernel start (mdp_device.h "register-resident layers"), so the
+// kernel pays one memory round trip, overlapped with the replay gather,
+// instead of one per layer; and each phase is given to the waves whose SIMDs
+// are free (waves w and w + 4 share a SIMD).  Workgroup barriers B1..B6 are
+// executed by every wave the same number of times, each role at its own point
+// of its program (a wave arrives late at a barrier when its own work there is
+// not needed by the others until the next one).
+//
+// k_critic_grad_r (maddpg.py:180-188):
+//   waves 0..na-1  target actor j -> Gumbel a~_j                 | B2
+//   wave 3         critic forward L1, L2                        | B2 | head q | B3
+//   waves 4..7     target-critic L1 column tile on obs' | B2 | + a~ part | B3 | L2 tile | B4
+//                  wave 4: head q', fp64 TD, dL/dq, d2, dW3, db3 | B5
+//   waves 0..3     dh1 tile = (d2 W2^T) o [h1 > 0]  ||  waves 4..7 dW2, db2 | B6
+//   all            dW1, db1
+// k_actor_grad_r (maddpg.py:37-58):
+//   wave 0  actor forward, Gumbel a_i                              | B2
+//   wave 1  critic L1 on the replay part (a_i rows masked) | B2 | + a_i part, L2, q, d2 | B3
+//   waves 4..7  dh1c tiles                                         | B4
+//   wave 0  da = dh1c W1c[a_i]^T, softmax backward + reg -> dlogits, d2a, dW3a, db3a | B5
+//   waves 0..3 dW2a, db2a  ||  waves 4..7 dh1a tiles               | B6
+//   all     dW1a, db1a
+#include "mdp_device.h"
+#include "mdp_kernels.h"
+
+namespace {
+constexpr int RH = MDP_RH, LH = MDP_RLH, LD = MDP_RLD;
+
+// column sums of a [16][ld] LDS block over the 64 columns, by the 64 lanes of one wave
+__device__ __forceinline__ void colsum64(const float* X, int ldx, float* __restrict__ out) {
+  const int c = threadIdx.x & 63;
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < MDP_R; ++r) s += X[r * ldx + c];
+  out[c] = s;
+}
+
+// dX tile (columns 16 tt .. 16 tt + 15) = (dY @ W^T) masked by Hin > 0
+__device__ __forceinline__ void dgrad_tile(const float* dY, const f32x4 (&w)[4], const float* Hin, float* dX, int tt) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const f32x4 acc = rdg_acc(dY, LD, w);
+  const int col = 16 * tt + r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = kq * 4 + i;
+    dX[row * LD + col] = Hin[row * LH + col] > 0.f ? acc[i] : 0.f;
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Topo& T = a.topo;
+  const ADesc& ag = T.ag[a.agent];
+  const NDesc& nd = ag.critic;
+  const bool lq = ag.local_q != 0;
+  const int na = lq ? 1 : T.n;
+  const int ldr = lds_ld(T.row_stride);
+  const int kb = MDP_ACT_DIM * na, ldA = lds_ld(kb);
+  const int ka_t = lq ? ag.obs_dim : T.sum_obs;  // target critic input part A: obs' (maddpg.py:86-87)
+  const int xo_t = lq ? ag.nobs_off : T.ag[0].nobs_off;
+  const int ka_c = lq ? ag.obs_dim : ag.cin;     // online critic input: the row prefix, or obs_i | act_i
+  const int xo_c = lq ? ag.obs_off : 0;
+  const int kb_c = lq ? MDP_ACT_DIM : 0;
+  LdsCarve cv(lds);
+  float* rowbuf = cv.take(MDP_R * ldr);
+  float* xa = cv.take(MDP_R * ldA);
+  float* lg = cv.take(3 * MDP_R * 8);
+  float* h1a = cv.take(3 * MDP_R * LH);
+  float* h2a = cv.take(3 * MDP_R * LH);
+  float* h1c = cv.take(MDP_R * LH);
+  float* h2c = cv.take(MDP_R * LH);
+  float* h1t = cv.take(MDP_R * LH);
+  float* h2t = cv.take(MDP_R * LH);
+  float* qv = cv.take(MDP_R);
+  float* qn = cv.take(MDP_R);
+  float* dq = cv.take(MDP_R);
+  float* d2 = cv.take(MDP_R * LD);
+  float* d1 = cv.take(MDP_R * LD);
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int r0 = blockIdx.x * MDP_R;
+  const int nvalid = min(MDP_R, a.B - r0);
+  const uint32_t ctr = a.ctl->upd_ctr;
+  const float* Pc = a.theta;
+  const float* Pt = a.target;
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
+  MDP_STAMP(0);
+
+  if (wave < 4) {
+    f32x4 wt[4];  // W2^T tile of the critic for dh1 (loaded once this wave's forward weights are dead)
+    if (wave < na) {
+      // ---------------- target actor j on obs'_j, Gumbel-softmax target action (maddpg.py:183)
+      const int j = lq ? a.agent : wave;
+      const ADesc& aj = T.ag[j];
+      const NDesc& an = aj.actor;
+      f32x4 w1[16], w2[16];
+      float w3[16];
+      rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
+      rf_load<16>(w2, Pt + an.t[2].off, RH, 0, 0);
+      rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
+      const f32x4 b1 = ld4(Pt + an.t[1].off + 4 * r), b2 = ld4(Pt + an.t[3].off + 4 * r);
+      const float b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
+      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+      __syncthreads();  // B1
+      MDP_STAMP(1);
+      float* h1 = h1a + wave * MDP_R * LH;
+      float* h2 = h2a + wave * MDP_R * LH;
+      float* lgj = lg + wave * MDP_R * 8;
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<16>(acc, rowbuf + aj.nobs_off, ldr, aj.obs_dim, w1);
+        rf_store<true>(acc, b1, h1, LH);
+      }
+      wave_sync();
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<16>(acc, h1, LH, RH, w2);
+        rf_store<true>(acc, b2, h2, LH);
+      }
+      wave_sync();
+      {
+        const f32x4 acc = rh_acc(h2, LH, w3);
+        if (r < MDP_ACT_DIM) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lgj[(kq * 4 + i) * 8 + r] = acc[i] + b3;
+        }
+      }
+      wave_sync();
+      if (lane < MDP_R) {  // distributions.py:264-266
+        const int row = lane;
+        float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
+        if (a.u_tgt) {
+          for (int k = 0; k < MDP_ACT_DIM; ++k)
+            u[k] = row < nvalid ? a.u_tgt[((int64_t)j * a.B + r0 + row) * MDP_ACT_DIM + k] : 0.5f;
+        } else {
+          uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + row), u);
+        }
+        gumbel_softmax5(lgj + row * 8, u, act);
+        const int dst = lq ? 0 : MDP_ACT_DIM * j;
+        for (int k = 0; k < MDP_ACT_DIM; ++k) xa[row * ldA + dst + k] = act[k];
+      }
+      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      __syncthreads();  // B2
+    } else if (wave == 3) {
+      // ---------------- online critic forward q(o, a) (maddpg.py:85-88, 104)
+      f32x4 w1[20], w1b[2], w2[16];
+      float w3[16];
+      rf_load<20>(w1, Pc + nd.t[0].off, ka_c, 0, 0);
+      rf_load<2>(w1b, Pc + nd.t[0].off + ka_c * RH, kb_c, 0, 0);
+      rf_load<16>(w2, Pc + nd.t[2].off, RH, 0, 0);
+      rq_load(w3, Pc + nd.t[4].off);
+      const f32x4 b1 = ld4(Pc + nd.t[1].off + 4 * r), b2 = ld4(Pc + nd.t[3].off + 4 * r);
+      const float b3 = Pc[nd.t[5].off];
+      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+      __syncthreads();  // B1
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<20>(acc, rowbuf + xo_c, ldr, ka_c, w1);
+        if (kb_c) rf_acc<2>(acc, rowbuf + ag.act_off, ldr, kb_c, w1b);
+        rf_store<true>(acc, b1, h1c, LH);
+      }
+      wave_sync();
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<16>(acc, h1c, LH, RH, w2);
+        rf_store<true>(acc, b2, h2c, LH);
+      }
+      wave_sync();
+      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      __syncthreads();  // B2
+      const float q = rq_head(h2c, LH, w3) + b3;
+      if ((lane & 3) == 0) qv[lane >> 2] = q;
+    } else {
+      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+      __syncthreads();  // B1
+      __syncthreads();  // B2
+    }
+    __syncthreads();  // B3
+    __syncthreads();  // B4
+    __syncthreads();  // B5: d2 ready
+    dgrad_tile(d2, wt, h1c, d1, wave);
+    __syncthreads();  // B6
+  } else {
+    // ---------------- target critic Q'(o', a~), one 16-column tile per wave
+    const int tt = wave - 4, col = 16 * tt + r;
+    float wa[16], wb[5], w2[16], w3[16];
+    rt_load<16>(wa, Pt + nd.t[0].off, RH, col, ka_t);
+    rt_load<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, kb);
+    rt_load<16>(w2, Pt + nd.t[2].off, RH, col, RH);
+    const float b1 = Pt[nd.t[1].off + col], b2 = Pt[nd.t[3].off + col];
+    if (tt == 0) rq_load(w3, Pt + nd.t[4].off);
+    const float b3 = Pt[nd.t[5].off];
+    const float w3c = Pc[nd.t[4].off + lane];  // d2 = dq * W3 of the online critic
+    gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+    __syncthreads();  // B1
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
+    __syncthreads();  // B2: a~ ready
+    MDP_STAMP(2);
+    rt_acc<5>(acc, xa, ldA, kb, wb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h1t[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b1, 0.f);
+    __syncthreads();  // B3
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    rt_acc<16>(acc, h1t, LH, RH, w2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h2t[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b2, 0.f);
+    __syncthreads();  // B4
+    MDP_STAMP(3);
+    if (tt == 0) {
+      // fp64 TD target (maddpg.py:186), loss partials, dL/dq = 2 (q - y) / B
+      const float qt = rq_head(h2t, LH, w3) + b3;
+      if ((lane & 3) == 0) qn[lane >> 2] = qt;
+      wave_sync();
+      double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;
+      float g = 0.f;
+      if (lane < nvalid) {
+        const double rew = (double)rowbuf[lane * ldr + ag.rew_off];
+        const double done = (double)rowbuf[lane * ldr + ag.done_off];
+        const double qnv = (double)qn[lane];
+        const double y64 = rew + a.gamma * (1.0 - done) * qnv;
+        const float y = (float)y64;
+        const float diff = qv[lane] - y;
+        g = (2.0f * diff) * a.inv_b;
+        s_l = (double)diff * (double)diff;
+        s_y = y64;
+        s_r = rew;
+        s_q = qnv;
+        a.y_out[r0 + lane] = y64;
+      }
+      if (lane < MDP_R) dq[lane] = g;
+      s_l = sum16(s_l);
+      s_y = sum16(s_y);
+      s_r = sum16(s_r);
+      s_q = sum16(s_q);
+      if (lane == 0) {
+        double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+        st[0] = s_l;
+        st[1] = s_y;
+        st[2] = s_r;
+        st[3] = s_q;
+      }
+      wave_sync();
+      // dW3 = h2^T dq, db3 = sum dq, d2 = (dq W3^T) o [h2 > 0]   (lane = hidden unit)
+      float s = 0.f, sb = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < MDP_R; ++rr) {
+        const float h = h2c[rr * LH + lane], dqr = dq[rr];
+        s = fmaf(h, dqr, s);
+        sb += dqr;
+        d2[rr * LD + lane] = h > 0.f ? dqr * w3c : 0.f;
+      }
+      slab[nd.t[4].off + lane] = s;
+      if (lane == 0) slab[nd.t[5].off] = sb;
+    }
+    __syncthreads();  // B5
+    MDP_STAMP(4);
+    // dW2 = h1^T d2 (waves 4..7), db2 = column sums of d2
+    wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 4, 4);
+    if (tt == 1) colsum64(d2, LD, slab + nd.t[3].off);
+    __syncthreads();  // B6
+  }
+  // dW1 = x^T dh1 over all waves, db1 = column sums of dh1
+  wgrad_waves(rowbuf + xo_c, ldr, ka_c, d1, LD, RH, slab + nd.t[0].off, 0, 8);
+  if (kb_c) wgrad_waves(rowbuf + ag.act_off, ldr, kb_c, d1, LD, RH, slab + nd.t[0].off + ka_c * RH, 0, 8);
+  if (wave == 7) colsum64(d1, LD, slab + nd.t[1].off);
+  MDP_STAMP(5);
+}
+
+__global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Topo& T = a.topo;
+  const ADesc& ag = T.ag[a.agent];
+  const NDesc& na = ag.actor;
+  const NDesc& nc = ag.critic;
+  const bool lq = ag.local_q != 0;
+  const int ldr = lds_ld(T.row_stride);
+  const int ka_c = lq ? ag.obs_dim : ag.cin;  // critic input from the replay row (a_i rows masked)
+  const int xo_c = lq ? ag.obs_off : 0;
+  LdsCarve cv(lds);
+  float* rowbuf = cv.take(MDP_R * ldr);
+  float* av = cv.take(MDP_R * 8);
+  float* lg = cv.take(MDP_R * 8);
+  float* da = cv.take(MDP_R * 8);
+  float* dl = cv.take(MDP_R * 8);
+  float* qv = cv.take(MDP_R);
+  float* h1a = cv.take(MDP_R * LH);
+  float* h2a = cv.take(MDP_R * LH);
+  float* h1c = cv.take(MDP_R * LH);
+  float* h2c = cv.take(MDP_R * LH);
+  float* d2c = cv.take(MDP_R * LD);
+  float* d1c = cv.take(MDP_R * LD);
+  float* d2a = cv.take(MDP_R * LD);
+  float* d1a = cv.take(MDP_R * LD);
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int r0 = blockIdx.x * MDP_R;
+  const int nvalid = min(MDP_R, a.B - r0);
+  const uint32_t ctr = a.ctl->upd_ctr;
+  const float* P = a.theta;
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
+  MDP_STAMP(0);
+
+  if (wave < 4) {
+    if (wave == 0) {
+      // ---------------- actor forward on obs_i -> logits p (maddpg.py:39), sample a_i (:49)
+      f32x4 w1[16], w2[16], wda[4];
+      float w3[16], w3a[MDP_ACT_DIM];
+      rf_load<16>(w1, P + na.t[0].off, ag.obs_dim, 0, 0);
+      rf_load<16>(w2, P + na.t[2].off, RH, 0, 0);
+      rh_load(w3, P + na.t[4].off, MDP_ACT_DIM);
+      const f32x4 b1 = ld4(P + na.t[1].off + 4 * r), b2 = ld4(P + na.t[3].off + 4 * r);
+      const float b3 = P[na.t[5].off + min(r, MDP_ACT_DIM - 1)];
+      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+      __syncthreads();  // B1
+      MDP_STAMP(1);
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<16>(acc, rowbuf + ag.obs_off, ldr, ag.obs_dim, w1);
+        rf_store<true>(acc, b1, h1a, LH);
+      }
+      wave_sync();
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<16>(acc, h1a, LH, RH, w2);
+        rf_store<true>(acc, b2, h2a, LH);
+      }
+      wave_sync();
+      {
+        const f32x4 acc = rh_acc(h2a, LH, w3);
+        if (r < MDP_ACT_DIM) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lg[(kq * 4 + i) * 8 + r] = acc[i] + b3;
+        }
+      }
+      wave_sync();
+      if (lane < MDP_R) {
+        float u[MDP_ACT_DIM];
+        if (a.u_act) {
+          for (int k = 0; k < MDP_ACT_DIM; ++k)
+            u[k] = lane < nvalid ? a.u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
+        } else {
+          uniforms5(a.seed, (uint32_t)((a.agent << 8) | 0x80), ctr, (uint32_t)(r0 + lane), u);
+        }
+        gumbel_softmax5(lg + lane * 8, u, av + lane * 8);
+      }
+      // backward-phase weights: W1c rows of the a_i input (for da) and W3 of the actor (for d2a)
+      rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
+#pragma unroll
+      for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
+      __syncthreads();  // B2: a_i ready
+      __syncthreads();  // B3: critic forward, d2c ready
+      __syncthreads();  // B4: dh1c ready
+      MDP_STAMP(2);
+      // da[r][k] = sum_h dh1c[r][h] W1c[a_in_off + k][h]
+      {
+        const f32x4 acc = rdg_acc(d1c, LD, wda);
+        if (r < MDP_ACT_DIM) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) da[(kq * 4 + i) * 8 + r] = acc[i];
+        }
+      }
+      wave_sync();
+      // softmax backward + regulariser: dlogits = (da - sum(a da)) a + reg 2 p / (B A); loss partials
+      double s_q = 0.0, s_p = 0.0;
+      if (lane < MDP_R) {
+        float dot = 0.f;
+        for (int k = 0; k < MDP_ACT_DIM; ++k) dot += da[lane * 8 + k] * av[lane * 8 + k];
+        for (int k = 0; k < MDP_ACT_DIM; ++k) {
+          const float g = (da[lane * 8 + k] - dot) * av[lane * 8 + k] + lg[lane * 8 + k] * a.reg_scale;
+          dl[lane * 8 + k] = lane < nvalid ? g : 0.f;
+        }
+        if (lane < nvalid) {
+          s_q = (double)qv[lane];
+          for (int k = 0; k < MDP_ACT_DIM; ++k) {
+            const double p = (double)lg[lane * 8 + k];
+            s_p += p * p;
+          }
+        }
+      }
+      s_q = sum16(s_q);
+      s_p = sum16(s_p);
+      if (lane == 0) {
+        double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+        st[0] = s_q;
+        st[1] = s_p;
+      }
+      wave_sync();
+      // dW3a = h2a^T dl, db3a, d2a = (dl W3a^T) o [h2a > 0]   (lane = hidden unit)
+      {
+        float gw[MDP_ACT_DIM] = {0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int rr = 0; rr < MDP_R; ++rr) {
+          const float h = h2a[rr * LH + lane];
+          float s = 0.f;
+#pragma unroll
+          for (int k = 0; k < MDP_ACT_DIM; ++k) {
+            const float d = dl[rr * 8 + k];
+            s = fmaf(d, w3a[k], s);
+            gw[k] = fmaf(h, d, gw[k]);
+          }
+          d2a[rr * LD + lane] = h > 0.f ? s : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < MDP_ACT_DIM; ++k) slab[na.t[4].off + lane * MDP_ACT_DIM + k] = gw[k];
+        if (lane < MDP_ACT_DIM) {
+          float s = 0.f;
+          for (int rr = 0; rr < MDP_R; ++rr) s += dl[rr * 8 + lane];
+          slab[na.t[5].off + lane] = s;
+        }
+      }
+      __syncthreads();  // B5: d2a ready
+    } else if (wave == 1) {
+      // ---------------- critic (post-step weights) forward with a_i = the sample (maddpg.py:48-52)
+      f32x4 w1[20], w1b[2], w2[16];
+      float w3[16];
+      rf_load<20>(w1, P + nc.t[0].off, ka_c, ag.a_in_off, ag.a_in_off + MDP_ACT_DIM);
+      rf_load<2>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM, 0, 0);
+      rf_load<16>(w2, P + nc.t[2].off, RH, 0, 0);
+      rq_load(w3, P + nc.t[4].off);
+      const f32x4 b1 = ld4(P + nc.t[1].off + 4 * r), b2 = ld4(P + nc.t[3].off + 4 * r);
+      const float b3 = P[nc.t[5].off];
+      const float w3c = P[nc.t[4].off + lane];
+      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+      __syncthreads();  // B1
+      f32x4 acc[4];
+      rf_zero(acc);
+      rf_acc<20>(acc, rowbuf + xo_c, ldr, ka_c, w1);
+      __syncthreads();  // B2
+      rf_acc<2>(acc, av, 8, MDP_ACT_DIM, w1b);
+      rf_store<true>(acc, b1, h1c, LH);
+      wave_sync();
+      rf_zero(acc);
+      rf_acc<16>(acc, h1c, LH, RH, w2);
+      rf_store<true>(acc, b2, h2c, LH);
+      wave_sync();
+      const float q = rq_head(h2c, LH, w3) + b3;
+      if ((lane & 3) == 0) qv[lane >> 2] = q;
+      // dL/dq = -1/B ; d2c = dq W3c masked by h2c > 0 (rows past the batch zero)
+#pragma unroll
+      for (int rr = 0; rr < MDP_R; ++rr)
+        d2c[rr * LD + lane] = (rr < nvalid && h2c[rr * LH + lane] > 0.f) ? a.neg_inv_b * w3c : 0.f;
+      __syncthreads();  // B3
+      __syncthreads();  // B4
+      __syncthreads();  // B5
+    } else {
+      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+      __syncthreads();  // B1
+      __syncthreads();  // B2
+      __syncthreads();  // B3
+      __syncthreads();  // B4
+      __syncthreads();  // B5
+    }
+    // dW2a = h1a^T d2a (waves 0..3), db2a
+    wgrad_waves(h1a, LH, RH, d2a, LD, RH, slab + na.t[2].off, 0, 4);
+    if (wave == 3) colsum64(d2a, LD, slab + na.t[3].off);
+    __syncthreads();  // B6
+  } else {
+    // ---------------- dgrad tiles: dh1c through the critic, dh1a through the actor
+    const int tt = wave - 4;
+    f32x4 wc[4], wa[4];
+    rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);
+    rdg_load(wa, P + na.t[2].off, 16 * tt + r, true);
+    gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+    __syncthreads();  // B1
+    __syncthreads();  // B2
+    __syncthreads();  // B3
+    dgrad_tile(d2c, wc, h1c, d1c, tt);
+    __syncthreads();  // B4
+    __syncthreads();  // B5
+    dgrad_tile(d2a, wa, h1a, d1a, tt);
+    __syncthreads();  // B6
+  }
+  // dW1a = obs_i^T dh1a over all waves, db1a
+  wgrad_waves(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1a, LD, RH, slab + na.t[0].off, 0, 8);
+  if (wave == 7) colsum64(d1a, LD, slab + na.t[1].off);
+  MDP_STAMP(3);
+}
+
+namespace {
+template <typename K, typename A>
+hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr) {
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, MDP_LDS_BUDGET);
+    (void)hipGetLastError();
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((a.B + MDP_R - 1) / MDP_R), dim3(512), lds, s, a);
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s) {
+  static bool attr = false;
+  return launch_r(k_critic_grad_r, a, lds_bytes, s, attr);
+}
+hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s) {
+  static bool attr = false;
+  return launch_r(k_actor_grad_r, a, lds_bytes, s, attr);
+}
+
+#ifdef MDP_STAMPS
+// diagnostic build: stamps of this translation unit's kernels (own code object)
+extern "C" int mdp_debug_stamps_r(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif

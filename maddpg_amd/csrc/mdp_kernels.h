@@ -147,6 +147,29 @@ inline int lds_actor_bytes(const Topo& t) {
   return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(S) + 5 * mdp_r4(R * 8));
 }
 #define MDP_LDS_BUDGET (160 * 1024)
+// fast (register-resident, H = 64) variants in mdp_grads_r.hip
+inline int lds_critic_r_bytes(const Topo& t, int agent) {
+  const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, LD = 65;
+  const int na = t.ag[agent].local_q ? 1 : t.n, ldA = mdp_ld(5 * na);
+  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldA) + 3 * R * 8 + 6 * R * LH + 4 * R * LH + 3 * R + 2 * mdp_r4(R * LD));
+}
+inline int lds_actor_r_bytes(const Topo& t) {
+  const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, LD = 65;
+  return 4 * (mdp_r4(R * ldr) + 4 * R * 8 + R + 4 * R * LH + 4 * mdp_r4(R * LD));
+}
+// the fast kernels hold every weight of a wave in registers: H = 64, at most 3
+// target actors, actor inputs <= 64, critic inputs <= 80, target-critic action part <= 20
+inline bool grads_r_ok(const Topo& t, int agent) {
+  if (t.H != 64) return false;
+  const ADesc& ag = t.ag[agent];
+  const int na = ag.local_q ? 1 : t.n;
+  if (na > 3) return false;
+  for (int j = 0; j < t.n; ++j)
+    if (t.ag[j].obs_dim > 64) return false;
+  if (ag.cin > 80) return false;
+  if ((ag.local_q ? ag.obs_dim : t.sum_obs) > 64) return false;
+  return 5 * na <= 20;
+}
 inline int lds_rollout_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), ldh = t.H + 1;
   return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8) + 2 * mdp_r4(R * 2 * MDP_MAX_ENT));
@@ -158,6 +181,8 @@ inline int lds_eval_bytes(int in, int H) {
 
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s);
+hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s);
+hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_rollout(const RolloutArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s);

@@ -179,6 +179,18 @@ def test_update_parity_tag6_h128():
     _update_parity([22, 22, 22, 22, 20, 20], B=256, L=1500, seed=25, H=128)
 
 
+def test_update_parity_tag4_h64_general_kernels():
+    # 4 target actors: outside the register-resident kernels' envelope -> general kernels
+    _update_parity([16, 16, 16, 14], B=512, L=2000, seed=26)
+
+
+@pytest.mark.parametrize("local_q", [None, [True, False, False]])
+def test_update_parity_general_kernels_forced(monkeypatch, local_q):
+    # the general kernels (mdp_grads.hip) on a configuration the fast ones also serve
+    monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
+    _update_parity([18, 18, 18], B=256, L=1200, seed=27, local_q=local_q)
+
+
 def test_update_round_uses_device_index_stream():
     """mdp_update_round draws agent 0's B indices first, then agent 1's ...
     (maddpg.py:167 per agent, train.py:160-161 agent order) from the MT stream."""
