@@ -27,9 +27,17 @@ __device__ unsigned long long g_mdp_stamps[64];
   do {                                                                                   \
     if (blockIdx.x == 0 && threadIdx.x == 0) g_mdp_stamps[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// stamp from lane 0 of whichever wave executes it (workgroup 0)
+#define MDP_STAMPW(i)                                                                              \
+  do {                                                                                             \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_mdp_stamps[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define MDP_STAMP(i) \
   do {               \
+  } while (0)
+#define MDP_STAMPW(i) \
+  do {                \
   } while (0)
 #endif
 
@@ -566,6 +574,23 @@ __device__ __forceinline__ void gather_rows16(const float* __restrict__ replay, 
   }
 }
 
+// the same over the threads [t0, t0 + nt) of the workgroup only
+__device__ __forceinline__ void gather_rows16_part(const float* __restrict__ replay, int stride,
+                                                   const int32_t* __restrict__ idx, int r0, int nvalid, float* rowbuf,
+                                                   int ldr, int t0, int nt) {
+  const int v4 = stride >> 2;
+  for (int e = (int)threadIdx.x - t0; e < MDP_R * v4; e += nt) {
+    const int r = e / v4, c4 = e - r * v4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < nvalid) v = *reinterpret_cast<const float4*>(replay + (int64_t)idx[r0 + r] * stride + c4 * 4);
+    float* d = rowbuf + r * ldr + c4 * 4;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+}
+
 __device__ __forceinline__ void copy_cols16(const float* src, int lds_src, int src_off, float* dst, int lds_dst, int dst_off,
                                    int ncols) {
   for (int e = threadIdx.x; e < MDP_R * ncols; e += blockDim.x) {
@@ -625,17 +650,20 @@ __device__ __forceinline__ void rf_load(f32x4 (&w)[KS], const float* __restrict_
   }
 }
 
-// acc[t] += X[16][K] @ W (the fragments of rf_load); X in LDS
+// acc[t] += X[16][K] @ W (the fragments of rf_load); X in LDS.  All A fragments
+// are read first (clamped, unconditional) so the MFMA chain never waits on LDS.
 template <int KS>
 __device__ __forceinline__ void rf_acc(f32x4 (&acc)[4], const float* X, int ldx, int K, const f32x4 (&w)[KS]) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const float* xr = X + r * ldx;
+  float x[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) x[s] = xr[min(4 * s + kq, K - 1)];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if (4 * s < K) {
-      const float x = xr[min(4 * s + kq, K - 1)];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x, w[s][t], acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s][t], acc[t], 0, 0, 0);
     }
   }
 }
@@ -670,9 +698,12 @@ __device__ __forceinline__ void rh_load(float (&w)[16], const float* __restrict_
 }
 __device__ __forceinline__ f32x4 rh_acc(const float* X, int ldx, const float (&w)[16]) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  float x[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) x[s] = X[r * ldx + 4 * s + kq];
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(X[r * ldx + 4 * s + kq], w[s], acc, 0, 0, 0);
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
   return acc;
 }
 
@@ -693,27 +724,28 @@ __device__ __forceinline__ float rq_head(const float* X, int ldx, const float (&
   return s;
 }
 
-// one 16-column tile per wave (column col = 16 tt + r of W[K][ldw]), k = 4s + kq
+// one 16-column tile per wave (column col = 16 tt + r of W[K][ldw]), k = 4s + kq;
+// unconditional clamped loads (straight-line code, exact vmcnt accounting); K >= 1
 template <int KS>
 __device__ __forceinline__ void rt_load(float (&w)[KS], const float* __restrict__ W, int ldw, int col, int K) {
   const int kq = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    w[s] = 0.f;
-    if (4 * s < K) {
-      const int k = 4 * s + kq;
-      const float v = W[min(k, K - 1) * ldw + col];
-      w[s] = k < K ? v : 0.f;
-    }
+    const int k = 4 * s + kq;
+    const float v = W[min(k, K - 1) * ldw + col];
+    w[s] = k < K ? v : 0.f;
   }
 }
 template <int KS>
 __device__ __forceinline__ void rt_acc(f32x4& acc, const float* X, int ldx, int K, const float (&w)[KS]) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const float* xr = X + r * ldx;
+  float x[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) x[s] = xr[min(4 * s + kq, K - 1)];
 #pragma unroll
   for (int s = 0; s < KS; ++s)
-    if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[min(4 * s + kq, K - 1)], w[s], acc, 0, 0, 0);
+    if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
 }
 
 // transposed tile for dX = dY @ W^T (W[K][64] row-major): output column kk = W row,
@@ -730,10 +762,25 @@ __device__ __forceinline__ void rdg_load(f32x4 (&w)[4], const float* __restrict_
 __device__ __forceinline__ f32x4 rdg_acc(const float* dY, int ldy, const f32x4 (&w)[4]) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const float* yr = dY + r * ldy + 16 * kq;
+  float x[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) x[s] = yr[s];
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(yr[s], w[s >> 2][s & 3], acc, 0, 0, 0);
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s >> 2][s & 3], acc, 0, 0, 0);
   return acc;
+}
+
+// LDS hand-off without a workgroup barrier: the producing waves signal after
+// their LDS writes completed; consumers spin (s_sleep) until every producer
+// has.  The counter must be zeroed before a barrier that precedes any signal.
+__device__ __forceinline__ void lds_signal(int* flag) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait(int* flag, int n) {
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < n) __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
 }
 
 // ------------------------------------------------ shared by the grad kernels

@@ -11,7 +11,10 @@
 // are free (waves w and w + 4 share a SIMD).  Workgroup barriers B1..B6 are
 // executed by every wave the same number of times, each role at its own point
 // of its program (a wave arrives late at a barrier when its own work there is
-// not needed by the others until the next one).
+// not needed by the others until the next one).  The replay rows are handed
+// over through an LDS counter instead of a barrier (B0 only zeroes it): the
+// waves with the heaviest weight loads never wait for the others to finish
+// ISSUING theirs (the per-CU load path is the prologue's bottleneck).
 //
 // k_critic_grad_r (maddpg.py:180-188):
 //   waves 0..na-1  target actor j -> Gumbel a~_j                 | B2
@@ -57,6 +60,7 @@ __device__ __forceinline__ void dgrad_tile(const float* dY, const f32x4 (&w)[4],
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ int rows_ready;  // gather waves done (LDS hand-off, replaces a barrier)
   const Topo& T = a.topo;
   const ADesc& ag = T.ag[a.agent];
   const NDesc& nd = ag.critic;
@@ -94,6 +98,8 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   const float* Pt = a.target;
   float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
   MDP_STAMP(0);
+  if (threadIdx.x == 0) rows_ready = 0;
+  __syncthreads();  // B0 (nothing in flight yet)
 
   if (wave < 4) {
     f32x4 wt[4];  // W2^T tile of the critic for dh1 (loaded once this wave's forward weights are dead)
@@ -102,6 +108,15 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       const int j = lq ? a.agent : wave;
       const ADesc& aj = T.ag[j];
       const NDesc& an = aj.actor;
+#ifdef MDP_STAMPS
+      MDP_STAMP(11);
+      {
+        volatile int sink = an.t[0].off + an.t[2].off;
+        (void)sink;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      MDP_STAMP(12);
+#endif
       f32x4 w1[16], w2[16];
       float w3[16];
       rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
@@ -109,8 +124,17 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
       const f32x4 b1 = ld4(Pt + an.t[1].off + 4 * r), b2 = ld4(Pt + an.t[3].off + 4 * r);
       const float b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
-      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-      __syncthreads();  // B1
+#ifdef MDP_STAMPS
+      MDP_STAMP(13);
+      {
+        float sink = w1[0][0] + w2[15][3] + w3[15] + b1[0] + b2[0] + b3;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        volatile float vs = sink;
+        (void)vs;
+      }
+      MDP_STAMP(14);
+#endif
+      lds_wait(&rows_ready, 4);
       MDP_STAMP(1);
       float* h1 = h1a + wave * MDP_R * LH;
       float* h2 = h2a + wave * MDP_R * LH;
@@ -150,6 +174,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         const int dst = lq ? 0 : MDP_ACT_DIM * j;
         for (int k = 0; k < MDP_ACT_DIM; ++k) xa[row * ldA + dst + k] = act[k];
       }
+      MDP_STAMP(2);
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       __syncthreads();  // B2
     } else if (wave == 3) {
@@ -162,8 +187,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       rq_load(w3, Pc + nd.t[4].off);
       const f32x4 b1 = ld4(Pc + nd.t[1].off + 4 * r), b2 = ld4(Pc + nd.t[3].off + 4 * r);
       const float b3 = Pc[nd.t[5].off];
-      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-      __syncthreads();  // B1
+      lds_wait(&rows_ready, 4);
       {
         f32x4 acc[4];
         rf_zero(acc);
@@ -179,14 +203,13 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         rf_store<true>(acc, b2, h2c, LH);
       }
       wave_sync();
+      MDP_STAMPW(3);
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       __syncthreads();  // B2
       const float q = rq_head(h2c, LH, w3) + b3;
       if ((lane & 3) == 0) qv[lane >> 2] = q;
     } else {
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
-      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-      __syncthreads();  // B1
       __syncthreads();  // B2
     }
     __syncthreads();  // B3
@@ -197,6 +220,16 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   } else {
     // ---------------- target critic Q'(o', a~), one 16-column tile per wave
     const int tt = wave - 4, col = 16 * tt + r;
+    // the replay gather is issued first, by these waves only (their own weights are few
+    // and needed late); waves 0..3 start on their weight loads at once
+    gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 256, 256);
+    lds_signal(&rows_ready);
+#ifdef MDP_STAMPS
+    if (tt == 0) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      MDP_STAMPW(15);
+    }
+#endif
     float wa[16], wb[5], w2[16], w3[16];
     rt_load<16>(wa, Pt + nd.t[0].off, RH, col, ka_t);
     rt_load<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, kb);
@@ -205,22 +238,22 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     if (tt == 0) rq_load(w3, Pt + nd.t[4].off);
     const float b3 = Pt[nd.t[5].off];
     const float w3c = Pc[nd.t[4].off + lane];  // d2 = dq * W3 of the online critic
-    gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-    __syncthreads();  // B1
+    lds_wait(&rows_ready, 4);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
     __syncthreads();  // B2: a~ ready
-    MDP_STAMP(2);
+    if (tt == 0) MDP_STAMPW(4);
     rt_acc<5>(acc, xa, ldA, kb, wb);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h1t[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b1, 0.f);
     __syncthreads();  // B3
+    if (tt == 0) MDP_STAMPW(5);
     acc = f32x4{0.f, 0.f, 0.f, 0.f};
     rt_acc<16>(acc, h1t, LH, RH, w2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h2t[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b2, 0.f);
     __syncthreads();  // B4
-    MDP_STAMP(3);
+    if (tt == 0) MDP_STAMPW(6);
     if (tt == 0) {
       // fp64 TD target (maddpg.py:186), loss partials, dL/dq = 2 (q - y) / B
       const float qt = rq_head(h2t, LH, w3) + b3;
@@ -266,23 +299,26 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       }
       slab[nd.t[4].off + lane] = s;
       if (lane == 0) slab[nd.t[5].off] = sb;
+      MDP_STAMPW(7);
     }
     __syncthreads();  // B5
-    MDP_STAMP(4);
+    if (tt == 0) MDP_STAMPW(8);
     // dW2 = h1^T d2 (waves 4..7), db2 = column sums of d2
     wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 4, 4);
     if (tt == 1) colsum64(d2, LD, slab + nd.t[3].off);
     __syncthreads();  // B6
+    if (tt == 0) MDP_STAMPW(9);
   }
   // dW1 = x^T dh1 over all waves, db1 = column sums of dh1
   wgrad_waves(rowbuf + xo_c, ldr, ka_c, d1, LD, RH, slab + nd.t[0].off, 0, 8);
   if (kb_c) wgrad_waves(rowbuf + ag.act_off, ldr, kb_c, d1, LD, RH, slab + nd.t[0].off + ka_c * RH, 0, 8);
   if (wave == 7) colsum64(d1, LD, slab + nd.t[1].off);
-  MDP_STAMP(5);
+  MDP_STAMP(10);
 }
 
 __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ int rows_ready;
   const Topo& T = a.topo;
   const ADesc& ag = T.ag[a.agent];
   const NDesc& na = ag.actor;
@@ -314,7 +350,9 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   const uint32_t ctr = a.ctl->upd_ctr;
   const float* P = a.theta;
   float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
-  MDP_STAMP(0);
+  MDP_STAMP(16);
+  if (threadIdx.x == 0) rows_ready = 0;
+  __syncthreads();  // B0
 
   if (wave < 4) {
     if (wave == 0) {
@@ -326,9 +364,8 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       rh_load(w3, P + na.t[4].off, MDP_ACT_DIM);
       const f32x4 b1 = ld4(P + na.t[1].off + 4 * r), b2 = ld4(P + na.t[3].off + 4 * r);
       const float b3 = P[na.t[5].off + min(r, MDP_ACT_DIM - 1)];
-      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-      __syncthreads();  // B1
-      MDP_STAMP(1);
+      lds_wait(&rows_ready, 6);
+      MDP_STAMP(17);
       {
         f32x4 acc[4];
         rf_zero(acc);
@@ -365,10 +402,11 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
 #pragma unroll
       for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
+      MDP_STAMP(18);
       __syncthreads();  // B2: a_i ready
       __syncthreads();  // B3: critic forward, d2c ready
       __syncthreads();  // B4: dh1c ready
-      MDP_STAMP(2);
+      MDP_STAMP(23);
       // da[r][k] = sum_h dh1c[r][h] W1c[a_in_off + k][h]
       {
         const f32x4 acc = rdg_acc(d1c, LD, wda);
@@ -425,6 +463,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
           slab[na.t[5].off + lane] = s;
         }
       }
+      MDP_STAMP(24);
       __syncthreads();  // B5: d2a ready
     } else if (wave == 1) {
       // ---------------- critic (post-step weights) forward with a_i = the sample (maddpg.py:48-52)
@@ -437,12 +476,12 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       const f32x4 b1 = ld4(P + nc.t[1].off + 4 * r), b2 = ld4(P + nc.t[3].off + 4 * r);
       const float b3 = P[nc.t[5].off];
       const float w3c = P[nc.t[4].off + lane];
-      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-      __syncthreads();  // B1
+      lds_wait(&rows_ready, 6);
       f32x4 acc[4];
       rf_zero(acc);
       rf_acc<20>(acc, rowbuf + xo_c, ldr, ka_c, w1);
       __syncthreads();  // B2
+      MDP_STAMPW(19);
       rf_acc<2>(acc, av, 8, MDP_ACT_DIM, w1b);
       rf_store<true>(acc, b1, h1c, LH);
       wave_sync();
@@ -456,12 +495,13 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
 #pragma unroll
       for (int rr = 0; rr < MDP_R; ++rr)
         d2c[rr * LD + lane] = (rr < nvalid && h2c[rr * LH + lane] > 0.f) ? a.neg_inv_b * w3c : 0.f;
+      MDP_STAMPW(20);
       __syncthreads();  // B3
       __syncthreads();  // B4
       __syncthreads();  // B5
     } else {
-      gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-      __syncthreads();  // B1
+      gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 128, 384);
+      lds_signal(&rows_ready);
       __syncthreads();  // B2
       __syncthreads();  // B3
       __syncthreads();  // B4
@@ -474,23 +514,28 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   } else {
     // ---------------- dgrad tiles: dh1c through the critic, dh1a through the actor
     const int tt = wave - 4;
+    // waves 2..7 gather the replay rows (first); waves 0, 1 start on their weights at once
+    gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 128, 384);
+    lds_signal(&rows_ready);
     f32x4 wc[4], wa[4];
     rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);
     rdg_load(wa, P + na.t[2].off, 16 * tt + r, true);
-    gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
-    __syncthreads();  // B1
     __syncthreads();  // B2
     __syncthreads();  // B3
+    if (tt == 0) MDP_STAMPW(21);
     dgrad_tile(d2c, wc, h1c, d1c, tt);
     __syncthreads();  // B4
+    if (tt == 0) MDP_STAMPW(22);
     __syncthreads();  // B5
+    if (tt == 0) MDP_STAMPW(25);
     dgrad_tile(d2a, wa, h1a, d1a, tt);
     __syncthreads();  // B6
+    if (tt == 0) MDP_STAMPW(26);
   }
   // dW1a = obs_i^T dh1a over all waves, db1a
   wgrad_waves(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1a, LD, RH, slab + na.t[0].off, 0, 8);
   if (wave == 7) colsum64(d1a, LD, slab + na.t[1].off);
-  MDP_STAMP(3);
+  MDP_STAMP(27);
 }
 
 namespace {

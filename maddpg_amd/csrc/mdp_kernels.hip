@@ -288,14 +288,28 @@ __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
     const TDesc td = a.net.t[t];
     const int n = td.rows * td.cols;
     const float* g = a.grad + td.off;
-    // all of this thread's loads are issued before the first is consumed
-    // (a rolled loop would pay one memory round trip per element)
+    // this block's chunk of grad / m / v / theta / target is requested together with
+    // the whole-tensor norm loads, so the block pays ONE memory round trip
+    constexpr int PT = MDP_APPLY_CHUNK / 256;  // parameters per thread
+    const int e0 = (b - a.blk[t]) * MDP_APPLY_CHUNK;
+    const int e1 = min(n, e0 + MDP_APPLY_CHUNK);
+    float cg[PT], cm[PT], cv[PT], cth[PT], ctg[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const int e = min(e0 + tid + q * 256, e1 - 1);
+      const int64_t i = td.off + e;
+      cg[q] = g[e];
+      cm[q] = a.m[i];
+      cv[q] = a.v[i];
+      cth[q] = a.theta[i];
+      ctg[q] = a.polyak ? a.target[i] : 0.f;
+    }
     double ss = 0.0;
-    for (int e0 = tid; e0 < n; e0 += 8 * blockDim.x) {
+    for (int f0 = tid; f0 < n; f0 += 8 * blockDim.x) {
       float v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int e = e0 + q * blockDim.x;
+        const int e = f0 + q * blockDim.x;
         v[q] = e < n ? g[min(e, n - 1)] * a.scale : 0.f;
       }
 #pragma unroll
@@ -308,18 +322,20 @@ __global__ __launch_bounds__(256) void k_apply(ApplyArgs a) {
     const float one = 1.0f;
     const float alpha = a.lr * sqrtf(one - b2p) / (one - b1p);
     const float c1 = one - a.b1, c2 = one - a.b2;
-    const int e0 = (b - a.blk[t]) * MDP_APPLY_CHUNK;
-    const int e1 = min(n, e0 + MDP_APPLY_CHUNK);
-    for (int e = e0 + tid; e < e1; e += blockDim.x) {
-      const int64_t i = td.off + e;
-      const float gc = ((g[e] * a.scale) * clip) / denom;
-      const float m = a.m[i] + (gc - a.m[i]) * c1;
-      const float v = a.v[i] + (gc * gc - a.v[i]) * c2;
-      const float th = a.theta[i] - (m * alpha) / (sqrtf(v) + a.eps);
-      a.m[i] = m;
-      a.v[i] = v;
-      a.theta[i] = th;
-      if (a.polyak) a.target[i] = a.pa * a.target[i] + a.pb * th;
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const int e = e0 + tid + q * 256;
+      if (e < e1) {
+        const int64_t i = td.off + e;
+        const float gc = ((cg[q] * a.scale) * clip) / denom;
+        const float m = cm[q] + (gc - cm[q]) * c1;
+        const float v = cv[q] + (gc * gc - cv[q]) * c2;
+        const float th = cth[q] - (m * alpha) / (sqrtf(v) + a.eps);
+        a.m[i] = m;
+        a.v[i] = v;
+        a.theta[i] = th;
+        if (a.polyak) a.target[i] = a.pa * ctg[q] + a.pb * th;
+      }
     }
   } else if (a.polyak && b < a.blk[6] + a.oblk[6]) {
     const int bb = b - a.blk[6];

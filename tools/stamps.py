@@ -21,19 +21,39 @@ eng.add_rows(torch.rand(30000, eng.row_stride))
 eng.init_params(0)
 eng.seed_py_random(0)
 lib = _lib.load()
-lib.mdp_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-names = {0: "start", 1: "gather+copies", 2: "tgt actors+critic fwd", 3: "tgt critic", 4: "TD,stats,dW3,d2",
-         5: "dh1,dW2,dW1"}
+fast = os.environ.get("MDP_GENERAL_GRADS") != "1"
+fn = lib.mdp_debug_stamps_r if fast else lib.mdp_debug_stamps
+fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 for it in range(5):
     eng.update_round()
     eng.synchronize()
 buf = (ctypes.c_ulonglong * 64)()
-lib.mdp_debug_stamps(buf, 64)
-st = np.array(buf[:6], dtype=np.int64)
-prev = st[0]
-for i in range(1, 6):
-    if st[i] == 0:
-        continue
-    print(f"{names.get(i, i):>14s}: {(st[i] - prev) * 10 / 1000:7.2f} us")
-    prev = st[i]
-print(f"{'total':>14s}: {(st[5] - st[0]) * 10 / 1000:7.2f} us")
+fn(buf, 64)
+st = np.array(buf[:], dtype=np.int64)
+if not fast:
+    names = {0: "start", 1: "gather+copies", 2: "tgt actors+critic fwd", 3: "tgt critic", 4: "TD,stats,dW3,d2",
+             5: "dh1,dW2,dW1"}
+    seq = [(0, 6)]
+else:
+    names = {0: "start", 1: "B1 gather+weights (w0)", 2: "tgt actor fwd+gumbel (w0)", 3: "critic L1+L2 (w3)",
+             4: "B2 (w4)", 5: "tgt L1 a~ part | B3 (w4)", 6: "tgt L2 tile | B4 (w4)", 7: "head, TD, d2 (w4)",
+             8: "B5 (w4)", 9: "dh1 tile, dW2 | B6 (w4)", 10: "dW1 end (w0)",
+             16: "start", 17: "B1 gather+weights (w0)", 18: "actor fwd+gumbel (w0)", 19: "B2 (w1)",
+             20: "critic fwd, d2c (w1)", 21: "B3 (w4)", 22: "dh1c tile | B4 (w4)", 23: "after B4 (w0)",
+             24: "da, softmax bwd, d2a (w0)", 25: "B5 (w4)", 26: "dh1a tile, dW2a | B6 (w4)", 27: "dW1a end (w0)"}
+    names.update({11: "role entry (w0)", 12: "kernarg chain (w0)", 13: "weights issued (w0)",
+                  14: "weights landed (w0)", 15: "gather landed (w4, from t=0)"})
+    seq = [(0, 11), (0, 1), (16, 28)]
+    prev = st[0]
+    for i in (11, 12, 13, 14, 15, 1):
+        print(f"{names[i]:>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us")
+        prev = st[i]
+    print()
+for lo, hi in seq:
+    prev = st[lo]
+    for i in range(lo + 1, hi):
+        if st[i] == 0:
+            continue
+        print(f"{names.get(i, i):>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us  (t={(st[i] - st[lo]) * 10 / 1000:6.2f})")
+        prev = st[i]
+    print()
