@@ -27,6 +27,11 @@ __device__ unsigned long long g_mdp_stamps[64];
   do {                                                                                   \
     if (blockIdx.x == 0 && threadIdx.x == 0) g_mdp_stamps[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// shader-clock stamp (s_memtime) next to the wall-clock ones, for the in-kernel clock
+#define MDP_CLK(i)                                                                      \
+  do {                                                                                  \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_mdp_stamps[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 // stamp from lane 0 of whichever wave executes it (workgroup 0)
 #define MDP_STAMPW(i)                                                                              \
   do {                                                                                             \
@@ -38,6 +43,9 @@ __device__ unsigned long long g_mdp_stamps[64];
   } while (0)
 #define MDP_STAMPW(i) \
   do {                \
+  } while (0)
+#define MDP_CLK(i) \
+  do {             \
   } while (0)
 #endif
 
@@ -253,12 +261,19 @@ __device__ __forceinline__ void tile_head(const float* X, int ldx, int K, const 
 }
 
 // softmax(logits - log(-log(u))) on one row of 5 (distributions.py:264-266)
-__device__ __forceinline__ void gumbel_softmax5(const float* logits, const float* u, float* a) {
+// Gumbel noise g = log(-log(u)) (distributions.py:235) -- independent of the
+// logits, so the fast kernels compute it while their weights are in flight
+__device__ __forceinline__ void gumbel_noise5(const float* u, float* gn) {
+#pragma unroll
+  for (int k = 0; k < MDP_ACT_DIM; ++k) gn[k] = logf(-logf(u[k]));
+}
+// softmax(logits - g): the same operations in the same order as gumbel_softmax5
+__device__ __forceinline__ void gumbel_softmax5_pre(const float* logits, const float* gn, float* a) {
   float z[MDP_ACT_DIM];
   float m = -INFINITY;
 #pragma unroll
   for (int k = 0; k < MDP_ACT_DIM; ++k) {
-    z[k] = logits[k] - logf(-logf(u[k]));
+    z[k] = logits[k] - gn[k];
     m = fmaxf(m, z[k]);
   }
   float s = 0.f;
@@ -269,6 +284,11 @@ __device__ __forceinline__ void gumbel_softmax5(const float* logits, const float
   }
 #pragma unroll
   for (int k = 0; k < MDP_ACT_DIM; ++k) a[k] = z[k] / s;
+}
+__device__ __forceinline__ void gumbel_softmax5(const float* logits, const float* u, float* a) {
+  float gn[MDP_ACT_DIM];
+  gumbel_noise5(u, gn);
+  gumbel_softmax5_pre(logits, gn, a);
 }
 
 // ------------------------------------------------------ phase-parallel tiles
@@ -659,6 +679,7 @@ __device__ __forceinline__ void rf_acc(f32x4 (&acc)[4], const float* X, int ldx,
   float x[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) x[s] = xr[min(4 * s + kq, K - 1)];
+  __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMA chain
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if (4 * s < K) {
@@ -701,6 +722,7 @@ __device__ __forceinline__ f32x4 rh_acc(const float* X, int ldx, const float (&w
   float x[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) x[s] = X[r * ldx + 4 * s + kq];
+  __builtin_amdgcn_sched_barrier(0);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
@@ -743,6 +765,7 @@ __device__ __forceinline__ void rt_acc(f32x4& acc, const float* X, int ldx, int 
   float x[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) x[s] = xr[min(4 * s + kq, K - 1)];
+  __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMA chain
 #pragma unroll
   for (int s = 0; s < KS; ++s)
     if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
@@ -765,6 +788,7 @@ __device__ __forceinline__ f32x4 rdg_acc(const float* dY, int ldy, const f32x4 (
   float x[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) x[s] = yr[s];
+  __builtin_amdgcn_sched_barrier(0);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s >> 2][s & 3], acc, 0, 0, 0);

@@ -124,6 +124,18 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
       const f32x4 b1 = ld4(Pt + an.t[1].off + 4 * r), b2 = ld4(Pt + an.t[3].off + 4 * r);
       const float b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
+      // Gumbel noise of the target action, computed while the weights are in flight
+      float gn[MDP_ACT_DIM];
+      {
+        float u[MDP_ACT_DIM];
+        if (a.u_tgt) {
+          for (int k = 0; k < MDP_ACT_DIM; ++k)
+            u[k] = lane < nvalid ? a.u_tgt[((int64_t)j * a.B + r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
+        } else {
+          uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
+        }
+        gumbel_noise5(u, gn);
+      }
 #ifdef MDP_STAMPS
       MDP_STAMP(13);
       {
@@ -136,6 +148,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 #endif
       lds_wait(&rows_ready, 4);
       MDP_STAMP(1);
+      MDP_CLK(40);
       float* h1 = h1a + wave * MDP_R * LH;
       float* h2 = h2a + wave * MDP_R * LH;
       float* lgj = lg + wave * MDP_R * 8;
@@ -146,6 +159,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         rf_store<true>(acc, b1, h1, LH);
       }
       wave_sync();
+      MDP_STAMP(41);
       {
         f32x4 acc[4];
         rf_zero(acc);
@@ -153,6 +167,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         rf_store<true>(acc, b2, h2, LH);
       }
       wave_sync();
+      MDP_STAMP(42);
       {
         const f32x4 acc = rh_acc(h2, LH, w3);
         if (r < MDP_ACT_DIM) {
@@ -161,20 +176,16 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         }
       }
       wave_sync();
+      MDP_STAMP(43);
       if (lane < MDP_R) {  // distributions.py:264-266
         const int row = lane;
-        float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
-        if (a.u_tgt) {
-          for (int k = 0; k < MDP_ACT_DIM; ++k)
-            u[k] = row < nvalid ? a.u_tgt[((int64_t)j * a.B + r0 + row) * MDP_ACT_DIM + k] : 0.5f;
-        } else {
-          uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + row), u);
-        }
-        gumbel_softmax5(lgj + row * 8, u, act);
+        float act[MDP_ACT_DIM];
+        gumbel_softmax5_pre(lgj + row * 8, gn, act);
         const int dst = lq ? 0 : MDP_ACT_DIM * j;
         for (int k = 0; k < MDP_ACT_DIM; ++k) xa[row * ldA + dst + k] = act[k];
       }
       MDP_STAMP(2);
+      MDP_CLK(44);
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       __syncthreads();  // B2
     } else if (wave == 3) {
@@ -364,6 +375,17 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       rh_load(w3, P + na.t[4].off, MDP_ACT_DIM);
       const f32x4 b1 = ld4(P + na.t[1].off + 4 * r), b2 = ld4(P + na.t[3].off + 4 * r);
       const float b3 = P[na.t[5].off + min(r, MDP_ACT_DIM - 1)];
+      float gn[MDP_ACT_DIM];  // Gumbel noise of the policy sample, while the weights are in flight
+      {
+        float u[MDP_ACT_DIM];
+        if (a.u_act) {
+          for (int k = 0; k < MDP_ACT_DIM; ++k)
+            u[k] = lane < nvalid ? a.u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
+        } else {
+          uniforms5(a.seed, (uint32_t)((a.agent << 8) | 0x80), ctr, (uint32_t)(r0 + (lane & 15)), u);
+        }
+        gumbel_noise5(u, gn);
+      }
       lds_wait(&rows_ready, 6);
       MDP_STAMP(17);
       {
@@ -388,16 +410,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
         }
       }
       wave_sync();
-      if (lane < MDP_R) {
-        float u[MDP_ACT_DIM];
-        if (a.u_act) {
-          for (int k = 0; k < MDP_ACT_DIM; ++k)
-            u[k] = lane < nvalid ? a.u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
-        } else {
-          uniforms5(a.seed, (uint32_t)((a.agent << 8) | 0x80), ctr, (uint32_t)(r0 + lane), u);
-        }
-        gumbel_softmax5(lg + lane * 8, u, av + lane * 8);
-      }
+      if (lane < MDP_R) gumbel_softmax5_pre(lg + lane * 8, gn, av + lane * 8);
       // backward-phase weights: W1c rows of the a_i input (for da) and W3 of the actor (for d2a)
       rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
 #pragma unroll

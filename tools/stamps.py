@@ -44,6 +44,10 @@ else:
     names.update({11: "role entry (w0)", 12: "kernarg chain (w0)", 13: "weights issued (w0)",
                   14: "weights landed (w0)", 15: "gather landed (w4, from t=0)"})
     seq = [(0, 11), (0, 1), (16, 28)]
+    print("actor fwd detail (w0): L1 %.2f  L2 %.2f  head %.2f  gumbel %.2f us" % tuple(
+        (st[b] - st[a]) * 10 / 1000 for a, b in ((1, 41), (41, 42), (42, 43), (43, 2))))
+    wall = (st[2] - st[1]) * 10e-9
+    print("in-kernel clock over the actor forward: %.3f GHz" % ((st[44] - st[40]) / wall / 1e9))
     prev = st[0]
     for i in (11, 12, 13, 14, 15, 1):
         print(f"{names[i]:>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us")
