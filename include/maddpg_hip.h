@@ -185,7 +185,8 @@ int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out_host);
 /* ---- profiling: HIP events bracketing every launch of one kernel kind -- */
 enum mdp_kernel_kind {
     MDP_K_INDEX = 0, MDP_K_GATHER = 1, MDP_K_CRITIC_GRAD = 2, MDP_K_ACTOR_GRAD = 3,
-    MDP_K_APPLY = 4, MDP_K_ROLLOUT = 5, MDP_K_REDUCE = 6, MDP_K_COUNT = 7
+    MDP_K_APPLY = 4, MDP_K_ROLLOUT = 5, MDP_K_REDUCE = 6, MDP_K_REDUCE_APPLY = 7,
+    MDP_K_COUNT = 8
 };
 int mdp_prof_enable(mdp_handle* h, int32_t kind, int32_t on);
 /* sum of event-measured durations (ms) and launch count since enable; synchronises */

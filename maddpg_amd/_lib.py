@@ -27,7 +27,7 @@ WHICH = {"actor": 0, "critic": 1, "tgt_actor": 2, "tgt_critic": 3, "m_actor": 4,
 REGION = {"theta": 0, "target": 1, "adam_m": 2, "adam_v": 3, "grad": 4, "replay": 5, "index": 6,
           "stats": 7, "env": 8, "eplog": 9, "beta": 10, "slab": 11, "ctl": 12}
 KERNEL = {"index": 0, "gather": 1, "critic_grad": 2, "actor_grad": 3, "apply": 4, "rollout": 5,
-          "reduce": 6}
+          "reduce": 6, "reduce_apply": 7}
 
 
 class MdpConfig(ctypes.Structure):

@@ -190,7 +190,8 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   sz[MDP_R_ENV] = (int64_t)E * (4 * 4 * L.n_ent + 4 + 4 + 4 * n) + 64;
   sz[MDP_R_EPLOG] = 4 * (int64_t)L.eplog_rows * (1 + n);
   sz[MDP_R_BETA] = 4 * 8 * (int64_t)n;  // per optimizer: next powers (TF vars), powers of this step
-  sz[MDP_R_SLAB] = 4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg + 8 * (int64_t)c->batch_size + 256;
+  sz[MDP_R_SLAB] = 4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg + 8 * (int64_t)c->batch_size + 256 +
+                   256 + mdp_ra_sync_bytes();
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
   for (int r = 0; r < MDP_R_COUNT; ++r) {
@@ -266,6 +267,10 @@ struct mdp_handle {
   // MDP_GENERAL_GRADS=1 in the environment at create: always use the general
   // grad kernels (mdp_grads.hip) -- lets tests compare both paths
   bool general_grads = false;
+  // single-GPU optimizer step as one k_reduce_apply launch (MDP_UNFUSED_APPLY=1: k_reduce + k_apply)
+  bool fused_apply = true;
+  uint32_t* ra_ctr = nullptr;
+  double* ra_part = nullptr;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
 };
@@ -429,7 +434,7 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
 }
 
 // net 1: critic Adam (+ critic stats); net 0: actor Adam + Polyak of both nets (+ actor stats)
-int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
+ApplyArgs apply_args(mdp_handle* h, int agent, int net, float scale) {
   const ADesc& ag = h->L.topo.ag[agent];
   ApplyArgs a;
   a.net = net ? ag.critic : ag.actor;
@@ -469,8 +474,39 @@ int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
   a.ticket = &h->ctl->ticket[net];
   a.ctl = h->ctl;
   a.bump_ctr = net ? 0 : 1;
+  return a;
+}
+
+int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
+  (void)from_slab;
+  const ApplyArgs a = apply_args(h, agent, net, scale);
   ProfScope p(h, MDP_K_APPLY);
   HIPCHK(h, mdp_launch_apply(a, h->stream));
+  return 0;
+}
+
+// batch reduction + clip + Adam (+ Polyak, stats, beta advance) in one launch
+// (single GPU); false when a tensor has more chunks than the sync area holds
+bool reduce_apply_ok(const mdp_handle* h, int agent, int net) {
+  const NDesc& d = net ? h->L.topo.ag[agent].critic : h->L.topo.ag[agent].actor;
+  for (int t = 0; t < 6; ++t)
+    if ((d.t[t].rows * d.t[t].cols + MDP_RA_CHUNK - 1) / MDP_RA_CHUNK > MDP_RA_MAXCH) return false;
+  return true;
+}
+
+int do_reduce_apply(mdp_handle* h, int agent, int net) {
+  FusedApplyArgs f;
+  f.ap = apply_args(h, agent, net, 1.0f);
+  f.ap.slab = net ? h->slab_c : h->slab_a;
+  f.rblk[0] = 0;
+  for (int t = 0; t < 6; ++t)
+    f.rblk[t + 1] = f.rblk[t] + (f.ap.net.t[t].rows * f.ap.net.t[t].cols + MDP_RA_CHUNK - 1) / MDP_RA_CHUNK;
+  const int g = agent * 2 + net;
+  f.sync_ctr = h->ra_ctr + (int64_t)g * 8 * 32;
+  f.done_ctr = f.sync_ctr + 6 * 32;
+  f.sync_part = h->ra_part + (int64_t)g * 6 * MDP_RA_MAXCH;
+  ProfScope p(h, MDP_K_REDUCE_APPLY);
+  HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
   return 0;
 }
 
@@ -495,12 +531,21 @@ int do_reduce(mdp_handle* h, int agent, int net) {
 
 int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act) {
   int rc;
+  const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
   if ((rc = do_critic_grad(h, agent, idx, u_tgt))) return rc;
-  if ((rc = do_reduce(h, agent, 1))) return rc;
-  if ((rc = do_apply(h, agent, 1, false, 1.0f))) return rc;
+  if (fused) {
+    if ((rc = do_reduce_apply(h, agent, 1))) return rc;
+  } else {
+    if ((rc = do_reduce(h, agent, 1))) return rc;
+    if ((rc = do_apply(h, agent, 1, false, 1.0f))) return rc;
+  }
   if ((rc = do_actor_grad(h, agent, idx, u_act))) return rc;
-  if ((rc = do_reduce(h, agent, 0))) return rc;
-  if ((rc = do_apply(h, agent, 0, false, 1.0f))) return rc;
+  if (fused) {
+    if ((rc = do_reduce_apply(h, agent, 0))) return rc;
+  } else {
+    if ((rc = do_reduce(h, agent, 0))) return rc;
+    if ((rc = do_apply(h, agent, 0, false, 1.0f))) return rc;
+  }
   return 0;
 }
 
@@ -540,6 +585,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
   {
     const char* g = getenv("MDP_GENERAL_GRADS");
     h->general_grads = g && g[0] == '1';
+    const char* u = getenv("MDP_UNFUSED_APPLY");
+    h->fused_apply = !(u && u[0] == '1');
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
@@ -594,6 +641,10 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->stat_a = (double*)p;
     p += 8 * 8 * nwg;
     h->y = (double*)p;
+    p += 8 * (int64_t)cfg->batch_size + 256;
+    p = (char*)(((uintptr_t)p + 255) & ~uintptr_t(255));
+    h->ra_ctr = (uint32_t*)p;
+    h->ra_part = (double*)(p + (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128);
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
   std::vector<float> beta(8 * cfg->n_agents);

@@ -78,6 +78,21 @@ struct ApplyArgs {
   int bump_ctr;
 };
 
+// k_reduce_apply (mdp_apply_fused.hip): batch reduction + optimizer step in one launch
+#define MDP_RA_CHUNK 256   // parameters per workgroup
+#define MDP_RA_MAXCH 256   // chunks per tensor the sync area holds
+struct FusedApplyArgs {
+  ApplyArgs ap;         // ap.slab / nwg / slab_stride: the partial gradients
+  int rblk[7];          // prefix counts of MDP_RA_CHUNK workgroups per tensor of ap.net
+  uint32_t* sync_ctr;   // 6 tensor counters of this (agent, net), 32 words apart
+  double* sync_part;    // [6][MDP_RA_MAXCH] published sums of squares
+  uint32_t* done_ctr;   // workgroups finished (last one advances beta)
+};
+// sync area: per (agent, net) 8 counters x 128 B, then [6][MAXCH] doubles
+inline int64_t mdp_ra_sync_bytes() {
+  return (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128 + (int64_t)MDP_MAX_AGENTS * 2 * 6 * MDP_RA_MAXCH * 8;
+}
+
 struct RolloutArgs {
   Topo topo;
   EnvDesc env;
@@ -187,6 +202,7 @@ hipError_t mdp_launch_rollout(const RolloutArgs& a, int H, int lds_bytes, hipStr
 hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s);
 hipError_t mdp_launch_reduce(const ReduceArgs& a, hipStream_t s);
+hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s);
 hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t s);
 hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
                              hipStream_t s);

@@ -211,6 +211,46 @@ def test_update_round_uses_device_index_stream():
         assert all(np.isfinite(eng.stats(i)))
 
 
+def _rounds_engine(dims, B, L, c, rounds):
+    eng = Engine(dims, batch_size=B, capacity=L)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    eng.init_params(7)
+    eng.seed_py_random(99)
+    for _ in range(rounds):
+        eng.update_round()
+    eng.synchronize()
+    return eng
+
+
+CTL_FAULT_OFFSET = 2572  # Ctl.fault (mdp_topo.h)
+
+
+def test_fused_reduce_apply_matches_two_kernel_path(monkeypatch):
+    """k_reduce_apply (one launch: batch reduction, cross-workgroup clip norm,
+    Adam, Polyak, beta advance) vs k_reduce + k_apply: same index/noise streams,
+    so one round agrees to fp32 summation order; 12 rounds: no spin timed out,
+    identical optimizer step counts."""
+    dims = [18, 18, 18]
+    B, L = 1024, 5000
+    c = synthetic_trainer_case(dims, B, L, seed=41)
+    fused1 = _rounds_engine(dims, B, L, c, 1)
+    fused12 = _rounds_engine(dims, B, L, c, 12)
+    monkeypatch.setenv("MDP_UNFUSED_APPLY", "1")
+    ref1 = _rounds_engine(dims, B, L, c, 1)
+    ref12 = _rounds_engine(dims, B, L, c, 12)
+    ctl = fused12.region("ctl", torch.uint8).cpu().numpy()
+    assert int(ctl[CTL_FAULT_OFFSET:CTL_FAULT_OFFSET + 4].view(np.uint32)[0]) == 0
+    for i in range(3):
+        for net in (0, 1):
+            np.testing.assert_array_equal(fused12.get_beta_powers(i, net), ref12.get_beta_powers(i, net))
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_actor", "v_critic"):
+            a, b = fused1.get_params(i, w), ref1.get_params(i, w)
+            for k in a:
+                np.testing.assert_allclose(a[k], b[k], rtol=0, atol=2e-4, err_msg=f"{i} {w} {k}")
+                assert np.all(np.isfinite(fused12.get_params(i, w)[k]))
+        np.testing.assert_allclose(fused1.stats(i), ref1.stats(i), rtol=1e-4, atol=1e-6)
+
+
 # --------------------------------------------------------------------- env
 SCENARIOS = [("simple", 1, 0), ("simple_spread", 3, 0), ("simple_adversary", 3, 1),
              ("simple_tag", 4, 3), ("simple_tag", 6, 4)]
