@@ -156,8 +156,15 @@ int mdp_update_gate(mdp_handle* h, int64_t t);
 /* update round: all agents in order (train.py:158-161), indices from the MT stream.
  * Replayed from a captured hipGraph after the first round (see mdp_set_graphs). */
 int mdp_update_round(mdp_handle* h);
-/* enable (default) / disable hipGraph replay of mdp_update_round */
+/* enable (default) / disable hipGraph replay of mdp_update_round / mdp_train_step */
 int mdp_set_graphs(mdp_handle* h, int32_t on);
+/* One vector step of the training loop (train.py:110-161 for num_envs env
+ * copies): mdp_env_step with the policy's own actions, then `rounds` update
+ * rounds (the rounds the update cadence makes due; 0..64).  Replayed as ONE
+ * hipGraph per distinct `rounds` (per-round graph launches leave the GPU idle
+ * between rounds).  Single-GPU path; data-parallel ranks use the phase entry
+ * points below with an all-reduce between them. */
+int mdp_train_step(mdp_handle* h, int32_t rounds);
 /* phase entry points for data parallelism (grad -> all-reduce -> apply) */
 int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev);
 int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev);

@@ -101,6 +101,7 @@ SIGNATURES = {
     "mdp_update_gate": (ctypes.c_int, [_P, _I64]),
     "mdp_update_round": (ctypes.c_int, [_P]),
     "mdp_set_graphs": (ctypes.c_int, [_P, _I32]),
+    "mdp_train_step": (ctypes.c_int, [_P, _I32]),
     "mdp_critic_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_actor_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_reduce_grad": (ctypes.c_int, [_P, _I32, _I32]),

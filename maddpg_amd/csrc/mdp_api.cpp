@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "mdp_kernels.h"
@@ -273,6 +274,9 @@ struct mdp_handle {
   double* ra_part = nullptr;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
+  // mdp_train_step graphs (rollout + k rounds), one per k
+  std::map<int, hipGraphExec_t> step_exec;
+  int eager_steps = 0;
 };
 
 namespace {
@@ -668,6 +672,7 @@ int mdp_destroy(mdp_handle* h) {
   for (int k = 0; k < MDP_K_COUNT; ++k)
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->round_exec) (void)hipGraphExecDestroy(h->round_exec);
+  for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
   if (h->round_graph) (void)hipGraphDestroy(h->round_graph);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -910,13 +915,18 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
   return do_update(h, agent, idx, u_tgt_dev, u_act_dev);
 }
 
+static int round_updates(mdp_handle* h, const int32_t* idx) {
+  const int n = h->cfg.n_agents, B = h->cfg.batch_size;
+  int rc = 0;
+  for (int i = 0; i < n && !rc; ++i) rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr);
+  return rc;
+}
+
 static int round_launches(mdp_handle* h) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   int rc = launch_make_index(h, n * B, h->index);
   if (rc) return rc;
-  for (int i = 0; i < n; ++i)
-    if ((rc = do_update(h, i, h->index + (int64_t)i * B, nullptr, nullptr))) return rc;
-  return 0;
+  return round_updates(h, h->index);
 }
 
 static bool any_prof(const mdp_handle* h) {
@@ -1013,8 +1023,7 @@ int mdp_env_reset(mdp_handle* h) {
   return 0;
 }
 
-int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
-  if (need_env(h)) return -1;
+static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
   RolloutArgs a;
   a.topo = h->L.topo;
   a.env = h->L.env;
@@ -1035,14 +1044,65 @@ int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
   a.act_in = act_in_dev;
   a.u_in = u_dev;
   a.ticket = &h->ctl->ticket[2];
-  {
-    ProfScope p(h, MDP_K_ROLLOUT);
-    HIPCHK(h, mdp_launch_rollout(a, h->cfg.num_units, lds_rollout_bytes(h->L.topo), h->stream));
-  }
+  ProfScope p(h, MDP_K_ROLLOUT);
+  HIPCHK(h, mdp_launch_rollout(a, h->cfg.num_units, lds_rollout_bytes(h->L.topo), h->stream));
+  return 0;
+}
+
+static void advance_ring_mirror(mdp_handle* h) {
   const int64_t cap = h->cfg.capacity, E = h->cfg.num_envs;
   h->len = std::min(cap, h->len + E);
   h->next = (h->next + E) % cap;
+}
+
+int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
+  if (need_env(h)) return -1;
+  const int rc = env_step_launch(h, act_in_dev, u_dev);
+  if (rc) return rc;
+  advance_ring_mirror(h);
   return 0;
+}
+
+static int step_launches(mdp_handle* h, int rounds) {
+  int rc = env_step_launch(h, nullptr, nullptr);
+  for (int r = 0; r < rounds && !rc; ++r) rc = round_launches(h);
+  return rc;
+}
+
+int mdp_train_step(mdp_handle* h, int32_t rounds) {
+  if (need_env(h)) return -1;
+  if (rounds < 0 || rounds > 64) return fail(h, "mdp_train_step: rounds must be in [0, 64]");
+  if (rounds > 0 && h->len + h->cfg.num_envs <= 0) return fail(h, "update round on an empty replay buffer");
+  int rc = 0;
+  // the index kernels read the ring length the rollout leaves (device Ctl); the
+  // host mirror moves first so the empty-buffer guard sees the same state
+  advance_ring_mirror(h);
+  if (!h->graphs || any_prof(h) || h->eager_steps < 1 || rounds == 0) {
+    if (rounds > 0) ++h->eager_steps;  // first training step eager (one-time kernel attribute setup)
+    rc = step_launches(h, rounds);
+  } else {
+    auto it = h->step_exec.find(rounds);
+    if (it == h->step_exec.end()) {
+      HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+      h->capturing = true;
+      rc = step_launches(h, rounds);
+      h->capturing = false;
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(h->stream, &g);
+      if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      if (e != hipSuccess) return fail(h, "hipStreamEndCapture", e);
+      hipGraphExec_t x = nullptr;
+      const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (ei != hipSuccess) return fail(h, "hipGraphInstantiate", ei);
+      it = h->step_exec.emplace(rounds, x).first;
+    }
+    HIPCHK(h, hipGraphLaunch(it->second, h->stream));
+  }
+  return rc;
 }
 
 int mdp_env_get_state(mdp_handle* h, float* pos, float* vel, int32_t* goal, int32_t* ep_step) {

@@ -332,6 +332,11 @@ class Engine:
     def update_round(self):
         self._c("mdp_update_round")
 
+    def train_step(self, rounds):
+        """one vector env step + `rounds` update rounds, as one graph replay
+        (mdp_train_step; single-GPU path)."""
+        self._c("mdp_train_step", int(rounds))
+
     def set_graphs(self, on=True):
         """hipGraph replay of update_round (default on; per-kernel profiling runs eager)."""
         self._c("mdp_set_graphs", 1 if on else 0)

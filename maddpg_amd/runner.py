@@ -67,6 +67,16 @@ class VecRunner:
 
     def step(self):
         t0 = self.train_step
+        if self.world_size == 1:
+            # rollout + the due rounds as one graph replay (mdp_train_step); the
+            # cadence is decided on the host from the ring mirror after this step
+            t1 = t0 + self.num_envs
+            len_after = min(self.eng.capacity, self.eng.buffer_len() + self.num_envs)
+            k = 0 if len_after < self.gate else rounds_due(t0, t1, self.train_every)
+            self.eng.train_step(k)
+            self.train_step = t1
+            self.rounds += k
+            return k
         self.rollout()
         k = self.due_rounds(t0, self.train_step)
         for _ in range(k):

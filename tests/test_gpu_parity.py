@@ -342,6 +342,36 @@ def test_rollout_policy_actions_match_oracle():
         np.testing.assert_allclose(rows[:, lay[j]["act"]:lay[j]["act"] + ACT], want, atol=2e-6)
 
 
+def test_train_step_graph_equals_step_then_rounds():
+    """mdp_train_step(k) (rollout + k rounds replayed as one graph) is the same
+    work as env_step + k x update_round: bit-identical state after 4 steps."""
+    from maddpg_amd.runner import VecRunner
+
+    def make():
+        r = VecRunner("simple_spread", 64, batch_size=128, capacity=20000, seed=3, train_every=16)
+        r.prefill()
+        return r
+
+    a, b = make(), make()
+    for _ in range(4):
+        t0 = a.train_step
+        k = a.step()                      # world 1: mdp_train_step
+        assert k == 4
+        b.rollout()
+        assert b.due_rounds(t0, b.train_step) == k
+        for _ in range(k):
+            b.train_round()
+    a.eng.synchronize()
+    b.eng.synchronize()
+    for i in range(3):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            pa, pb = a.eng.get_params(i, w), b.eng.get_params(i, w)
+            for key in pa:
+                np.testing.assert_array_equal(pa[key], pb[key])
+    np.testing.assert_array_equal(a.eng.replay_rows(0, 2000).cpu().numpy(), b.eng.replay_rows(0, 2000).cpu().numpy())
+    assert a.eng.buffer_len() == b.eng.buffer_len()
+
+
 # ---------------------------------------------------- size-independent checks
 def test_full_size_index_stream_properties():
     """BASELINE S3-sized draw (1e6-row ring, 6 x 4096 indices): bit-exact vs
