@@ -165,6 +165,18 @@ int mdp_set_graphs(mdp_handle* h, int32_t on);
  * between rounds).  Single-GPU path; data-parallel ranks use the phase entry
  * points below with an all-reduce between them. */
 int mdp_train_step(mdp_handle* h, int32_t rounds);
+
+/* ---- native data parallelism (one process per GPU, RCCL over xGMI) ------
+ * Replaces the reference's single-process update (maddpg.py:161-196) on G
+ * ranks: each rank owns its env copies / replay shard / index stream; every
+ * optimizer phase sums the reduced gradient with one ncclAllReduce on the
+ * engine stream and applies it x 1/G (SURVEY §8e strict mode).  Rank 0 makes
+ * the id, the caller broadcasts it (e.g. torch.distributed), every rank calls
+ * mdp_dp_init; afterwards mdp_update / mdp_update_round / mdp_train_step run
+ * the data-parallel update (collectives launched eagerly; MDP_DP_GRAPHS=1 in
+ * the environment captures them in the step graph). RCCL is dlopen'ed. */
+int mdp_dp_unique_id(uint8_t* out128);
+int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank);
 /* phase entry points for data parallelism (grad -> all-reduce -> apply) */
 int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev);
 int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev);

@@ -12,6 +12,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <map>
 #include <vector>
 
@@ -277,6 +280,10 @@ struct mdp_handle {
   // mdp_train_step graphs (rollout + k rounds), one per k
   std::map<int, hipGraphExec_t> step_exec;
   int eager_steps = 0;
+  // native data parallelism (mdp_dp_init): RCCL communicator of this rank
+  ncclComm_t comm = nullptr;
+  int dp_world = 1;
+  bool dp_graphs = false;  // capture collectives in the step graph (MDP_DP_GRAPHS=1)
 };
 
 namespace {
@@ -533,7 +540,62 @@ int do_reduce(mdp_handle* h, int agent, int net) {
   return 0;
 }
 
+// ---- RCCL, loaded on first use (the library has no link-time RCCL dependency)
+struct RcclApi {
+  bool tried = false, ok = false;
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) err = nullptr;
+};
+RcclApi& rccl() {
+  static RcclApi r;
+  if (!r.tried) {
+    r.tried = true;
+    void* so = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!so) so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (so) {
+      r.get_id = (decltype(r.get_id))dlsym(so, "ncclGetUniqueId");
+      r.init_rank = (decltype(r.init_rank))dlsym(so, "ncclCommInitRank");
+      r.all_reduce = (decltype(r.all_reduce))dlsym(so, "ncclAllReduce");
+      r.destroy = (decltype(r.destroy))dlsym(so, "ncclCommDestroy");
+      r.err = (decltype(r.err))dlsym(so, "ncclGetErrorString");
+      r.ok = r.get_id && r.init_rank && r.all_reduce && r.destroy && r.err;
+    }
+  }
+  return r;
+}
+
+// sum all-reduce of one net's reduced gradient (flat, in the grad region) on the engine stream
+int dp_allreduce(mdp_handle* h, int agent, int net) {
+  const NDesc& d = net_of(h, agent, net);
+  float* g = h->grad + d.off;
+  const ncclResult_t r = rccl().all_reduce(g, g, (size_t)d.size, ncclFloat32, ncclSum, h->comm, h->stream);
+  if (r != ncclSuccess) {
+    h->err = std::string("ncclAllReduce: ") + rccl().err(r);
+    return -1;
+  }
+  return 0;
+}
+
+// strict data-parallel update of one agent (maddpg.py:188-194 order):
+// critic grads -> reduce -> all-reduce -> clip + Adam (x 1/G); then the actor
+int do_update_dp(mdp_handle* h, int agent, const int32_t* idx) {
+  const float scale = 1.0f / (float)h->dp_world;
+  int rc;
+  if ((rc = do_critic_grad(h, agent, idx, nullptr))) return rc;
+  if ((rc = do_reduce(h, agent, 1))) return rc;
+  if ((rc = dp_allreduce(h, agent, 1))) return rc;
+  if ((rc = do_apply(h, agent, 1, false, scale))) return rc;
+  if ((rc = do_actor_grad(h, agent, idx, nullptr))) return rc;
+  if ((rc = do_reduce(h, agent, 0))) return rc;
+  if ((rc = dp_allreduce(h, agent, 0))) return rc;
+  return do_apply(h, agent, 0, false, scale);
+}
+
 int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act) {
+  if (h->comm && !u_tgt && !u_act) return do_update_dp(h, agent, idx);
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
   if ((rc = do_critic_grad(h, agent, idx, u_tgt))) return rc;
@@ -672,6 +734,7 @@ int mdp_destroy(mdp_handle* h) {
   for (int k = 0; k < MDP_K_COUNT; ++k)
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->round_exec) (void)hipGraphExecDestroy(h->round_exec);
+  if (h->comm) (void)rccl().destroy(h->comm);
   for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
   if (h->round_graph) (void)hipGraphDestroy(h->round_graph);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -964,6 +1027,45 @@ int mdp_update_round(mdp_handle* h) {
   return 0;
 }
 
+int mdp_dp_unique_id(uint8_t* out128) {
+  if (!out128 || !rccl().ok) return -1;
+  ncclUniqueId id;
+  if (rccl().get_id(&id) != ncclSuccess) return -1;
+  std::memcpy(out128, &id, sizeof(id));
+  return 0;
+}
+
+int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank) {
+  if (!h || !id128) return -1;
+  if (!rccl().ok) return fail(h, "librccl.so.1 could not be loaded");
+  if (world < 1 || rank < 0 || rank >= world) return fail(h, "mdp_dp_init: bad world/rank");
+  if (h->comm) return fail(h, "mdp_dp_init: already initialised");
+  ncclUniqueId id;
+  std::memcpy(&id, id128, sizeof(id));
+  HIPCHK(h, hipSetDevice(h->device));
+  const ncclResult_t r = rccl().init_rank(&h->comm, world, id, rank);
+  if (r != ncclSuccess) {
+    h->comm = nullptr;
+    h->err = std::string("ncclCommInitRank: ") + rccl().err(r);
+    return -1;
+  }
+  h->dp_world = world;
+  const char* g = getenv("MDP_DP_GRAPHS");
+  h->dp_graphs = g && g[0] == '1';
+  // drop graphs captured without the collectives
+  for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
+  h->step_exec.clear();
+  if (h->round_exec) {
+    (void)hipGraphExecDestroy(h->round_exec);
+    h->round_exec = nullptr;
+  }
+  if (h->round_graph) {
+    (void)hipGraphDestroy(h->round_graph);
+    h->round_graph = nullptr;
+  }
+  return 0;
+}
+
 int mdp_set_graphs(mdp_handle* h, int32_t on) {
   h->graphs = on != 0;
   return 0;
@@ -1077,7 +1179,8 @@ int mdp_train_step(mdp_handle* h, int32_t rounds) {
   // the index kernels read the ring length the rollout leaves (device Ctl); the
   // host mirror moves first so the empty-buffer guard sees the same state
   advance_ring_mirror(h);
-  if (!h->graphs || any_prof(h) || h->eager_steps < 1 || rounds == 0) {
+  const bool no_graph = h->comm && !h->dp_graphs;  // collectives launched eagerly unless asked
+  if (!h->graphs || no_graph || any_prof(h) || h->eager_steps < 1 || rounds == 0) {
     if (rounds > 0) ++h->eager_steps;  // first training step eager (one-time kernel attribute setup)
     rc = step_launches(h, rounds);
   } else {

@@ -337,6 +337,37 @@ class Engine:
         (mdp_train_step; single-GPU path)."""
         self._c("mdp_train_step", int(rounds))
 
+    def dp_init(self, world, rank, uid=None):
+        """Native data parallelism: join an RCCL communicator of `world` ranks
+        (mdp_dp_init).  `uid` (128 bytes) comes from rank 0's dp_unique_id();
+        with torch.distributed initialised, dp_init_from_dist() shares it."""
+        if uid is None:
+            uid = Engine.dp_unique_id()
+        self._c("mdp_dp_init", bytes(uid), int(world), int(rank))
+
+    @staticmethod
+    def dp_unique_id():
+        buf = ctypes.create_string_buffer(128)
+        if _lib.load().mdp_dp_unique_id(buf) != 0:
+            raise _lib.MdpError("mdp_dp_unique_id failed (librccl.so.1 not loadable?)")
+        return buf.raw
+
+    def dp_init_from_dist(self, world, rank):
+        """rank 0 makes the RCCL id, torch.distributed broadcasts it, every rank
+        joins; returns False on every rank if rank 0 could not make one."""
+        import torch.distributed as dist
+        obj = [None]
+        if rank == 0:
+            try:
+                obj[0] = Engine.dp_unique_id()
+            except Exception:
+                obj[0] = None
+        dist.broadcast_object_list(obj, src=0)
+        if obj[0] is None:
+            return False
+        self.dp_init(world, rank, obj[0])
+        return True
+
     def set_graphs(self, on=True):
         """hipGraph replay of update_round (default on; per-kernel profiling runs eager)."""
         self._c("mdp_set_graphs", 1 if on else 0)

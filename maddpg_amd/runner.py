@@ -10,6 +10,7 @@ by E per vector step, so a round runs for every multiple of 100 crossed
 applies unchanged.  Index draws, gathers, both optimiser steps and Polyak
 updates run on the device in the reference's agent order.
 """
+import os
 from . import envs
 from .engine import Engine
 from .parallel import EngineOps, make_allreduce, strict_round
@@ -48,6 +49,12 @@ class VecRunner:
         self.rounds = 0
         self._ops = EngineOps(self.eng) if world_size > 1 else None
         self._allreduce = make_allreduce(self.eng.stream) if world_size > 1 else None
+        # native data parallelism: the library's own RCCL communicator, so a whole
+        # vector step (rollout + due rounds with their all-reduces) is one C call;
+        # MDP_NATIVE_DP=0 keeps the torch.distributed path (strict_round)
+        self.native_dp = False
+        if world_size > 1 and os.environ.get("MDP_NATIVE_DP", "1") == "1":
+            self.native_dp = self.eng.dp_init_from_dist(world_size, rank)
 
     def rollout(self):
         self.eng.env_step()
@@ -67,7 +74,7 @@ class VecRunner:
 
     def step(self):
         t0 = self.train_step
-        if self.world_size == 1:
+        if self.world_size == 1 or self.native_dp:
             # rollout + the due rounds as one graph replay (mdp_train_step); the
             # cadence is decided on the host from the ring mirror after this step
             t1 = t0 + self.num_envs
