@@ -65,11 +65,21 @@ def roofline_for(kind, eng, ms_avg):
         f = flops_critic_grad if kind == "critic_grad" else flops_actor_grad
         fl = sum(f(eng, i) for i in range(eng.n)) / eng.n
         ach = fl / (ms_avg * 1e-3) / 1e12
+        suffix = "_r" if eng.lib.mdp_grad_variant(eng.h, 0) == 1 else ""
         return {"bound": "mfma", "achieved": round(ach, 4), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 6), "traffic": None,
-                "kernel": f"k_{kind}", "algorithmic_per_launch": fl, "avg_launch_ms": ms_avg}
+                "kernel": f"k_{kind}{suffix}", "algorithmic_per_launch": fl, "avg_launch_ms": ms_avg}
     if kind == "rollout":
         by = bytes_rollout(eng)
+    elif kind == "reduce_apply":
+        # per launch (critic and actor launches alternate): the nwg partial
+        # gradients + m, v, theta (read + write) + grad write + target (actor)
+        H, o = eng.num_units, eng.obs_dims
+        pa = sum(d * H + H + H * H + H + 5 * H + 5 for d in o) / eng.n
+        cin = sum(o) + 5 * eng.n
+        pc = cin * H + H + H * H + H + H + 1
+        nwg = (eng.batch_size + 15) // 16
+        by = 4 * ((pc + pa) / 2) * (nwg + 7) + 4 * pa
     else:
         return None
     ach = by / (ms_avg * 1e-3) / 1e9
@@ -176,6 +186,22 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # second figure: rollout only (actors + Gumbel + MPE physics + replay
+    # append) over the same env copies, no training
+    ro_steps = max(10, args.steps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(ro_steps):
+        r.rollout()
+    torch.cuda.synchronize()
+    ro_dt = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([ro_dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ro_dt = float(t.item())
+    rollout_only = args.num_envs * ro_steps * world / ro_dt
     # Kernel timing pass: the same workload again with a HIP event pair around
     # every launch of every kernel kind on the engine stream (this forces the
     # eager launch path; the timed region above replays the captured round graph).
@@ -189,8 +215,9 @@ def main():
     for k in kinds:
         eng.prof_enable(k, False)
     # the dominant kernel among those with a roofline model (grads: MFMA, rollout: HBM)
-    modelled = [k for k in ("critic_grad", "actor_grad", "rollout") if per_kind[k][1]]
-    dominant = max(modelled, key=lambda k: per_kind[k][0]) if modelled else None
+    modelled = [k for k in ("critic_grad", "actor_grad", "rollout", "reduce_apply") if per_kind[k][1]]
+    ev_pre = event_overhead_ms(eng.stream)
+    dominant = max(modelled, key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_pre) if modelled else None
     ms_tot, launches = per_kind[dominant] if dominant else (0.0, 0)
 
     env_steps = args.num_envs * args.steps * world
@@ -201,7 +228,8 @@ def main():
     if launches:
         raw = ms_tot / launches
         roof = roofline_for(dominant, eng, max(raw - ev_ms, 1e-6))
-        roof["dominant_of_all_kinds"] = max(per_kind, key=lambda k: per_kind[k][0])
+        roof["dominant_of_all_kinds"] = max(
+            (k for k in per_kind if per_kind[k][1]), key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_ms)
         roof["avg_launch_ms_raw_events"] = raw
         roof["event_pair_overhead_ms"] = ev_ms
         roof["launches_timed"] = launches
@@ -230,7 +258,10 @@ def main():
                        "global_batch": args.batch_size * world, "parallelism": f"dp{world}",
                        "mode": "rollout-only" if args.rollout_only else "strict"},
             "trainer_updates_per_sec": round(updates / dt, 3),
+            "rounds_per_sec": round(rounds / dt, 3),
+            "rollout_only_env_steps_per_sec": round(rollout_only, 3),
             "update_rounds": rounds,
+            "dp": ("native-rccl" if getattr(r, "native_dp", False) else "torch.distributed") if world > 1 else None,
             "kernel_pass": {"steps": prof_steps, "event_pair_overhead_ms": round(ev_ms, 5),
                             "per_kind_ms_per_launch": {k: round(v[0] / v[1] - ev_ms, 5) for k, v in per_kind.items()
                                                        if v[1]},

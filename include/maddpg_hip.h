@@ -208,6 +208,9 @@ enum mdp_kernel_kind {
     MDP_K_COUNT = 8
 };
 int mdp_prof_enable(mdp_handle* h, int32_t kind, int32_t on);
+/* which grad kernels serve `agent`: 1 = register-resident k_*_grad_r (H = 64
+ * envelope), 0 = general k_*_grad */
+int mdp_grad_variant(mdp_handle* h, int32_t agent);
 /* sum of event-measured durations (ms) and launch count since enable; synchronises */
 int mdp_prof_read(mdp_handle* h, int32_t kind, double* total_ms, int64_t* launches);
 

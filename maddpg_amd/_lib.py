@@ -103,6 +103,7 @@ SIGNATURES = {
     "mdp_set_graphs": (ctypes.c_int, [_P, _I32]),
     "mdp_train_step": (ctypes.c_int, [_P, _I32]),
     "mdp_dp_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "mdp_grad_variant": (ctypes.c_int, [_P, _I32]),
     "mdp_dp_init": (ctypes.c_int, [_P, ctypes.c_char_p, _I32, _I32]),
     "mdp_critic_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_actor_grad": (ctypes.c_int, [_P, _I32, _P, _P]),

@@ -1027,6 +1027,11 @@ int mdp_update_round(mdp_handle* h) {
   return 0;
 }
 
+int mdp_grad_variant(mdp_handle* h, int32_t agent) {
+  if (!h || agent < 0 || agent >= h->cfg.n_agents) return -1;
+  return (!h->general_grads && grads_r_ok(h->L.topo, agent)) ? 1 : 0;
+}
+
 int mdp_dp_unique_id(uint8_t* out128) {
   if (!out128 || !rccl().ok) return -1;
   ncclUniqueId id;
