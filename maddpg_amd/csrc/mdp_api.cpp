@@ -189,7 +189,7 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   int64_t sz[MDP_R_COUNT];
   sz[MDP_R_THETA] = sz[MDP_R_TARGET] = sz[MDP_R_ADAM_M] = sz[MDP_R_ADAM_V] = sz[MDP_R_GRAD] = 4 * L.PT;
   sz[MDP_R_REPLAY] = 4 * c->capacity * T.row_stride;
-  sz[MDP_R_INDEX] = 4 * (int64_t)n * c->batch_size;
+  sz[MDP_R_INDEX] = 2 * 4 * (int64_t)n * c->batch_size;  // two slots: round r draws round r+1's
   sz[MDP_R_STATS] = 8 * 8 * (int64_t)n;
   sz[MDP_R_ENV] = (int64_t)E * (4 * 4 * L.n_ent + 4 + 4 + 4 * n) + 64;
   sz[MDP_R_EPLOG] = 4 * (int64_t)L.eplog_rows * (1 + n);
@@ -386,8 +386,11 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
   return 0;
 }
 
-int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt) {
+int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr) {
   CriticArgs a;
+  a.pf_ctl = h->ctl;
+  a.pf_out = nullptr;
+  a.pf_count = 0;
   a.topo = h->L.topo;
   a.agent = agent;
   a.B = h->cfg.batch_size;
@@ -406,6 +409,10 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.y_out = h->y;
   ProfScope p(h, MDP_K_CRITIC_GRAD);
   if (!h->general_grads && grads_r_ok(h->L.topo, agent)) {
+    if (pf_out) {
+      a.pf_out = pf_out;
+      a.pf_count = h->cfg.n_agents * h->cfg.batch_size;
+    }
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
     return 0;
   }
@@ -581,10 +588,10 @@ int dp_allreduce(mdp_handle* h, int agent, int net) {
 
 // strict data-parallel update of one agent (maddpg.py:188-194 order):
 // critic grads -> reduce -> all-reduce -> clip + Adam (x 1/G); then the actor
-int do_update_dp(mdp_handle* h, int agent, const int32_t* idx) {
+int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out) {
   const float scale = 1.0f / (float)h->dp_world;
   int rc;
-  if ((rc = do_critic_grad(h, agent, idx, nullptr))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out))) return rc;
   if ((rc = do_reduce(h, agent, 1))) return rc;
   if ((rc = dp_allreduce(h, agent, 1))) return rc;
   if ((rc = do_apply(h, agent, 1, false, scale))) return rc;
@@ -594,11 +601,13 @@ int do_update_dp(mdp_handle* h, int agent, const int32_t* idx) {
   return do_apply(h, agent, 0, false, scale);
 }
 
-int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act) {
-  if (h->comm && !u_tgt && !u_act) return do_update_dp(h, agent, idx);
+// pf_out: the critic kernel also draws the next round's indices there (fast path only)
+int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act,
+              int32_t* pf_out = nullptr) {
+  if (h->comm && !u_tgt && !u_act) return do_update_dp(h, agent, idx, pf_out);
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
-  if ((rc = do_critic_grad(h, agent, idx, u_tgt))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out))) return rc;
   if (fused) {
     if ((rc = do_reduce_apply(h, agent, 1))) return rc;
   } else {
@@ -978,11 +987,16 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
   return do_update(h, agent, idx, u_tgt_dev, u_act_dev);
 }
 
-static int round_updates(mdp_handle* h, const int32_t* idx) {
+static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nullptr) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   int rc = 0;
-  for (int i = 0; i < n && !rc; ++i) rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr);
+  for (int i = 0; i < n && !rc; ++i) rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, i == 0 ? pf_out : nullptr);
   return rc;
+}
+
+// can agent 0's critic kernel draw the next round's indices on the side?
+static bool prefetch_ok(const mdp_handle* h) {
+  return !h->general_grads && grads_r_ok(h->L.topo, 0) && h->cfg.n_agents * h->cfg.batch_size <= 4096;
 }
 
 static int round_launches(mdp_handle* h) {
@@ -1170,9 +1184,22 @@ int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
   return 0;
 }
 
+// rollout, then `rounds` rounds on alternating index slots; round r's first
+// critic kernel draws round r+1's indices (same ring length: the rounds of one
+// step follow one rollout) in an extra workgroup -- the draw leaves the
+// critical path for every round but the first
 static int step_launches(mdp_handle* h, int rounds) {
   int rc = env_step_launch(h, nullptr, nullptr);
-  for (int r = 0; r < rounds && !rc; ++r) rc = round_launches(h);
+  if (rc || rounds == 0) return rc;
+  const int nb = h->cfg.n_agents * h->cfg.batch_size;
+  int32_t* slot[2] = {h->index, h->index + nb};
+  const bool pf = prefetch_ok(h);
+  if ((rc = launch_make_index(h, nb, slot[0]))) return rc;
+  for (int r = 0; r < rounds && !rc; ++r) {
+    const bool more = r + 1 < rounds;
+    rc = round_updates(h, slot[r & 1], (more && pf) ? slot[(r + 1) & 1] : nullptr);
+    if (!rc && more && !pf) rc = launch_make_index(h, nb, slot[(r + 1) & 1]);
+  }
   return rc;
 }
 

@@ -32,6 +32,7 @@
 //   all     dW1a, db1a
 #include "mdp_device.h"
 #include "mdp_kernels.h"
+#include "mdp_mt.h"
 
 namespace {
 constexpr int RH = MDP_RH, LH = MDP_RLH, LD = MDP_RLD;
@@ -59,6 +60,12 @@ __device__ __forceinline__ void dgrad_tile(const float* dY, const f32x4 (&w)[4],
 }  // namespace
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
+  if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
+    // the next round's index draw (same ring length, the MT stream continues):
+    // one workgroup beside the B/16 of this kernel, so it costs no time of its own
+    make_index_block<512>(a.pf_ctl, a.pf_count, a.pf_out);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;  // gather waves done (LDS hand-off, replaces a barrier)
   const Topo& T = a.topo;
@@ -553,20 +560,20 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
 
 namespace {
 template <typename K, typename A>
-hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr) {
+hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr, int extra = 0) {
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, MDP_LDS_BUDGET);
     (void)hipGetLastError();
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3((a.B + MDP_R - 1) / MDP_R), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(kern, dim3((a.B + MDP_R - 1) / MDP_R + extra), dim3(512), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace
 
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s) {
   static bool attr = false;
-  return launch_r(k_critic_grad_r, a, lds_bytes, s, attr);
+  return launch_r(k_critic_grad_r, a, lds_bytes, s, attr, a.pf_count > 0 ? 1 : 0);
 }
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s) {
   static bool attr = false;

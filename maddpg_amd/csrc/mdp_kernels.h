@@ -22,6 +22,11 @@ struct CriticArgs {
   double* slab_stat;    // [nwg][8]
   double* y_out;        // [B]
   int group;            // target actors run concurrently per pass (LDS budget)
+  // k_critic_grad_r only: one extra workgroup draws the NEXT round's indices
+  // (pf_count draws into pf_out) while this kernel runs (0: none)
+  Ctl* pf_ctl;
+  int32_t* pf_out;
+  int pf_count;
 };
 
 struct ActorArgs {

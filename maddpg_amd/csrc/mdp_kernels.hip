@@ -11,108 +11,15 @@
 //                                        + replay append + episode reset), k_env_reset
 #include "mdp_device.h"
 #include "mdp_kernels.h"
+#include "mdp_mt.h"
 
 // ================================================================ index
-namespace {
-
-__device__ inline uint32_t mt_temper(uint32_t y) {
-  y ^= y >> 11;
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
-  y ^= y >> 18;
-  return y;
-}
-
-__device__ inline uint32_t mt_mix(uint32_t cur, uint32_t nxt) {
-  const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
-  return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-}
-
-// MT19937 generation step over 624 words in LDS, in 4 dependency stages.
-// Sequential form: for kk in 0..623: mt[kk] = mt[(kk+397)%624] ^ mix(mt[kk], mt[kk+1])
-// kk <  227 reads old mt[kk+397]; 227 <= kk < 623 reads new mt[kk-227]; kk = 623
-// reads new mt[396] and new mt[0].
-__device__ void mt_twist(uint32_t* mt) {
-  const int t = threadIdx.x;
-  uint32_t cur = 0, nxt = 0, far = 0;
-  if (t < 624) {
-    cur = mt[t];
-    nxt = mt[t + 1 < 624 ? t + 1 : 0];
-  }
-  if (t < 227) far = mt[t + 397];
-  __syncthreads();
-  if (t < 227) mt[t] = far ^ mt_mix(cur, nxt);
-  __syncthreads();
-  if (t >= 227 && t < 454) mt[t] = mt[t - 227] ^ mt_mix(cur, nxt);
-  __syncthreads();
-  if (t >= 454 && t < 623) mt[t] = mt[t - 227] ^ mt_mix(cur, nxt);
-  __syncthreads();
-  if (t == 623) mt[623] = mt[396] ^ mt_mix(cur, mt[0]);
-  __syncthreads();
-}
-
-}  // namespace
-
 // count x randint(0, len-1): r = getrandbits(k) = temper(next) >> (32-k),
 // k = len.bit_length(), rejected while r >= len (Lib/random.py _randbelow).
 // Accepted draws are compacted with a workgroup prefix sum; the stream
-// position after the count-th accepted draw is stored back.
+// position after the count-th accepted draw is stored back (mdp_mt.h).
 __global__ __launch_bounds__(1024) void k_make_index(Ctl* ctl, int count, int32_t* __restrict__ out) {
-  __shared__ uint32_t mt[624];
-  __shared__ int wsum[16];
-  __shared__ int s_newpos;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  for (int i = t; i < 624; i += blockDim.x) mt[i] = ctl->mt[i];
-  int pos = ctl->mt_pos;
-  const uint32_t n = (uint32_t)ctl->len;
-  if (n == 0) {  // randint(0, -1) raises in the reference; the host refuses it too
-    for (int i = t; i < count; i += blockDim.x) out[i] = 0;
-    return;
-  }
-  const int k = 32 - __clz(n);
-  __syncthreads();
-  int produced = 0;
-  // acceptance >= 1/2 per draw, so ~count/312 passes; the bound only guards a hang
-  const int max_iters = 64 + count / 64;
-  int iters = 0;
-  while (produced < count && iters++ < max_iters) {
-    if (pos >= 624) {
-      mt_twist(mt);
-      pos = 0;
-    }
-    const int avail = 624 - pos;
-    bool acc = false;
-    uint32_t r = 0;
-    if (t < avail) {
-      r = mt_temper(mt[pos + t]) >> (32 - k);
-      acc = r < n;
-    }
-    const unsigned long long bal = __ballot(acc);
-    const int wrank = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[w] = __popcll(bal);
-    __syncthreads();
-    int before = 0, total = 0;
-    for (int i = 0; i < 16; ++i) {
-      const int c = wsum[i];
-      before += (i < w) ? c : 0;
-      total += c;
-    }
-    const int rank = before + wrank;
-    const int need = count - produced;
-    if (acc && rank < need) out[produced + rank] = (int32_t)r;
-    if (total >= need) {
-      if (acc && rank == need - 1) s_newpos = pos + t + 1;
-      __syncthreads();
-      pos = s_newpos;
-      produced = count;
-    } else {
-      produced += total;
-      pos = 624;
-    }
-    __syncthreads();
-  }
-  for (int i = t; i < 624; i += blockDim.x) ctl->mt[i] = mt[i];
-  if (t == 0) ctl->mt_pos = pos;
+  make_index_block<1024>(ctl, count, out);
 }
 
 // ================================================================ replay
