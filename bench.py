@@ -149,14 +149,23 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rollout-only", action="store_true", help="time env steps without training")
+    # BASELINE configs[3]/[4]: simple_adversary with mixed maddpg/ddpg policies, simple_tag N=6
+    ap.add_argument("--num-agents", type=int, default=None, help="scenario agent count override")
+    ap.add_argument("--scenario-adversaries", type=int, default=None, help="adversaries in the scenario world")
+    ap.add_argument("--num-adversaries", type=int, default=0, help="agents trained with --adv-policy")
+    ap.add_argument("--good-policy", default="maddpg")
+    ap.add_argument("--adv-policy", default="maddpg")
     args = ap.parse_args()
 
     world, rank, local = init_process_group_from_env()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     torch.cuda.set_device(local)
-    r = VecRunner(args.scenario, args.num_envs, batch_size=args.batch_size, num_units=args.num_units,
-                  seed=args.seed, train_every=args.train_every, world_size=world, rank=rank)
+    r = VecRunner(args.scenario, args.num_envs, n_agents=args.num_agents,
+                  scenario_adversaries=args.scenario_adversaries, num_adversaries=args.num_adversaries,
+                  good_policy=args.good_policy, adv_policy=args.adv_policy, batch_size=args.batch_size,
+                  num_units=args.num_units, seed=args.seed, train_every=args.train_every, world_size=world,
+                  rank=rank)
     eng = r.eng
     r.prefill()
     kinds = [k for k in _lib.KERNEL]
@@ -234,12 +243,15 @@ def main():
         roof["event_pair_overhead_ms"] = ev_ms
         roof["launches_timed"] = launches
     cfg_key = f"{args.scenario}_E{args.num_envs}_B{args.batch_size}_H{args.num_units}"
+    if args.num_agents is not None:
+        cfg_key += f"_N{args.num_agents}"
     if roof is not None:
         tr = load_traffic(roof["kernel"], cfg_key)
         roof["traffic"] = tr
     if rank == 0:
         out = {
-            "metric": "env-steps/sec (end-to-end at the reference update cadence), simple_spread N=3, batch 1024",
+            "metric": (f"env-steps/sec (end-to-end at the reference update cadence), {args.scenario} N={r.n}, "
+                       f"batch {args.batch_size}"),
             "value": round(value, 3),
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -253,7 +265,9 @@ def main():
             "data": "synthetic (random-init weights, device MPE env rollouts)",
             "config": {"workload": f"{args.scenario} N={r.n}, {args.num_envs} env copies per GPU, batch "
                                    f"{args.batch_size}, {args.num_units}-unit MLPs, 1 update round per "
-                                   f"{args.train_every} transitions per rank",
+                                   f"{args.train_every} transitions per rank"
+                                   + (f", policies {['ddpg' if q else 'maddpg' for q in eng.local_q]}"
+                                      if any(eng.local_q) else ""),
                        "scenario": args.scenario, "num_envs_per_gpu": args.num_envs,
                        "global_batch": args.batch_size * world, "parallelism": f"dp{world}",
                        "mode": "rollout-only" if args.rollout_only else "strict"},

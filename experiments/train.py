@@ -66,6 +66,47 @@ def parse_args(argv=None):
     return parser.parse_args(argv)
 
 
+def benchmark(arglist, runner, exp_name, rank):
+    """--benchmark (train.py:139-148): run the loaded policies, record every
+    agent's scenario benchmark_data() each step, no training.  The reference
+    keeps ``agent_info`` = one entry per episode, each ``[[info_n['n'] per
+    step]]``; a reset appends the new entry BEFORE the step's info is stored,
+    so an episode's terminal-step record opens the next entry, and the dump
+    (once train_step > --benchmark-iters at a terminal step) drops the last
+    entry.  With E env copies every copy keeps its own episode stream; the
+    pickle lists episodes in (episode, env copy) order.  E=1 is the reference
+    structure exactly."""
+    from maddpg_amd.envs import bench_record
+    eng, sp, n = runner.eng, runner.spec, runner.n
+    E, L = arglist.num_envs, arglist.max_episode_len
+    if sp.name == "simple":
+        raise AttributeError("'Scenario' object has no attribute 'benchmark_data' (scenario simple)")
+    open_eps = [[[]] for _ in range(E)]
+    closed = []
+    train_step = 0
+    vec_steps = 0
+    while True:
+        info = eng.env_step_bench().cpu().numpy()        # [E, n, BENCH_W]
+        vec_steps += 1
+        train_step += E
+        terminal = vec_steps % L == 0
+        if terminal:
+            closed.extend(open_eps)
+            open_eps = [[[]] for _ in range(E)]
+        for e in range(E):
+            open_eps[e][0].append([bench_record(sp, info[e, i], i) for i in range(n)])
+        if train_step > arglist.benchmark_iters and terminal:
+            if rank == 0:
+                file_name = arglist.benchmark_dir + exp_name + '.pkl'
+                print('Finished benchmarking, now saving...', flush=True)
+                os.makedirs(os.path.dirname(file_name) or ".", exist_ok=True)
+                with open(file_name, 'wb') as fp:
+                    pickle.dump(closed, fp)
+            break
+    runner.synchronize()
+    return runner
+
+
 def train(arglist):
     import torch
 
@@ -74,8 +115,6 @@ def train(arglist):
 
     if arglist.display:
         raise SystemExit("--display needs MPE's pyglet viewer, which this build does not ship")
-    if arglist.benchmark:
-        raise SystemExit("--benchmark (scenario benchmark_data) is not implemented in this round")
     exp_name = arglist.exp_name if arglist.exp_name is not None else arglist.scenario
     world, rank, local = init_process_group_from_env()
     if torch.cuda.is_available():
@@ -94,9 +133,11 @@ def train(arglist):
 
     if arglist.load_dir == "":
         arglist.load_dir = arglist.save_dir
-    if arglist.restore:
+    if arglist.restore or arglist.benchmark:                  # train.py:92-96
         say('Loading previous state...')
         runner.eng.load_state(arglist.load_dir)
+    if arglist.benchmark:
+        return benchmark(arglist, runner, exp_name, rank)
 
     E, L = arglist.num_envs, arglist.max_episode_len
     final_ep_rewards, final_ep_ag_rewards = [], []

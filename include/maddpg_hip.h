@@ -197,6 +197,16 @@ int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev);
 int mdp_env_get_state(mdp_handle* h, float* pos_host, float* vel_host, int32_t* goal_host, int32_t* ep_step_host);
 int mdp_env_set_state(mdp_handle* h, const float* pos_host, const float* vel_host, const int32_t* goal_host, const int32_t* ep_step_host);
 int mdp_env_obs(mdp_handle* h, float* obs_dev);   /* current obs [E][sum obs] */
+/* --benchmark mode (train.py:139-148): mdp_env_step that also writes every
+ * agent's scenario benchmark_data() of the post-physics state (MPE
+ * environment._get_info -> info_n['n']) to info_dev [E][n][MDP_BENCH_W] fp32,
+ * before the episode reset.  Record per scenario (zero-padded):
+ *   simple_spread    (rew_i, collisions_i, sum_l min_a dist, occupied landmarks)
+ *   simple_adversary adversary: (|pos - goal|^2); good: (|pos - lm_l|^2 ..., |pos - goal|^2)
+ *   simple_tag       adversary: (good agents in contact); good: (0)
+ *   simple           has no benchmark_data (the reference's make_env raises): error */
+#define MDP_BENCH_W 8
+int mdp_env_step_bench(mdp_handle* h, float* info_dev);
 /* finished-episode log: total entries written so far, copy last `n` [n][1+n_agents] */
 int64_t mdp_episode_count(mdp_handle* h);
 int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out_host);

@@ -20,6 +20,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "maddpg_hip.h")
 
 MAX_AGENTS = 8
 ACT_DIM = 5
+BENCH_W = 8   # MDP_BENCH_W: floats per agent benchmark_data record
 
 SCN = {"none": 0, "simple": 1, "simple_spread": 2, "simple_adversary": 3, "simple_tag": 4}
 WHICH = {"actor": 0, "critic": 1, "tgt_actor": 2, "tgt_critic": 3, "m_actor": 4, "v_actor": 5,
@@ -115,6 +116,7 @@ SIGNATURES = {
     "mdp_env_get_state": (ctypes.c_int, [_P, _F32P, _F32P, _I32P, _I32P]),
     "mdp_env_set_state": (ctypes.c_int, [_P, _F32P, _F32P, _I32P, _I32P]),
     "mdp_env_obs": (ctypes.c_int, [_P, _P]),
+    "mdp_env_step_bench": (ctypes.c_int, [_P, _P]),
     "mdp_episode_count": (_I64, [_P]),
     "mdp_episode_log": (ctypes.c_int, [_P, _I64, _I64, _F32P]),
     "mdp_prof_enable": (ctypes.c_int, [_P, _I32, _I32]),

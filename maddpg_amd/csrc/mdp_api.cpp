@@ -1144,7 +1144,7 @@ int mdp_env_reset(mdp_handle* h) {
   return 0;
 }
 
-static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
+static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* u_dev, float* bench = nullptr) {
   RolloutArgs a;
   a.topo = h->L.topo;
   a.env = h->L.env;
@@ -1165,6 +1165,7 @@ static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* 
   a.act_in = act_in_dev;
   a.u_in = u_dev;
   a.ticket = &h->ctl->ticket[2];
+  a.bench = bench;
   ProfScope p(h, MDP_K_ROLLOUT);
   HIPCHK(h, mdp_launch_rollout(a, h->cfg.num_units, lds_rollout_bytes(h->L.topo), h->stream));
   return 0;
@@ -1179,6 +1180,17 @@ static void advance_ring_mirror(mdp_handle* h) {
 int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
   if (need_env(h)) return -1;
   const int rc = env_step_launch(h, act_in_dev, u_dev);
+  if (rc) return rc;
+  advance_ring_mirror(h);
+  return 0;
+}
+
+int mdp_env_step_bench(mdp_handle* h, float* info_dev) {
+  if (need_env(h)) return -1;
+  if (!info_dev) return fail(h, "mdp_env_step_bench: info_dev is null");
+  if (h->cfg.scenario == MDP_SCN_SIMPLE)
+    return fail(h, "scenario 'simple' has no benchmark_data (MPE Scenario attribute missing)");
+  const int rc = env_step_launch(h, nullptr, nullptr, info_dev);
   if (rc) return rc;
   advance_ring_mirror(h);
   return 0;

@@ -117,6 +117,7 @@ struct RolloutArgs {
   const float* act_in;
   const float* u_in;
   uint32_t* ticket;
+  float* bench;  // benchmark_data records [E][n][MDP_BENCH_W] or null
 };
 
 struct EnvResetArgs {

@@ -457,6 +457,65 @@ __device__ inline void env_reward(const EnvDesc& E, const float* p, int goal, fl
   }
 }
 
+// scenario benchmark_data() of every agent (MPE environment._get_info with
+// info_callback = scenario.benchmark_data, train.py:57-60,139-141) into
+// out[n][MDP_BENCH_W], zero-padded.  Same post-physics state as env_reward.
+__device__ inline void env_bench(const EnvDesc& E, const float* p, int goal, float* out) {
+  const int n = E.n_agents, L = E.n_landmarks;
+  for (int q = 0; q < n * MDP_BENCH_W; ++q) out[q] = 0.f;
+  switch (E.scenario) {
+    case MDP_SCN_SPREAD: {
+      float min_dists = 0.f, occupied = 0.f;
+      for (int l = 0; l < L; ++l) {
+        float m = INFINITY;
+        for (int a = 0; a < n; ++a) m = fminf(m, dist2(p, a, n + l));
+        min_dists += m;
+        if (m < 0.1f) occupied += 1.f;
+      }
+      for (int i = 0; i < n; ++i) {
+        float coll = 0.f;
+        for (int a = 0; a < n; ++a)
+          if (dist2(p, a, i) < E.size[a] + E.size[i]) coll += 1.f;  // includes self
+        float* o = out + i * MDP_BENCH_W;
+        o[0] = -min_dists - coll;
+        o[1] = coll;
+        o[2] = min_dists;
+        o[3] = occupied;
+      }
+      break;
+    }
+    case MDP_SCN_ADVERSARY: {
+      const int g = n + goal;
+      for (int i = 0; i < n; ++i) {
+        float* o = out + i * MDP_BENCH_W;
+        auto sq = [&](int b) {
+          const float dx = p[2 * i] - p[2 * b], dy = p[2 * i + 1] - p[2 * b + 1];
+          return dx * dx + dy * dy;
+        };
+        if (E.adversary[i]) {
+          o[0] = sq(g);
+        } else {
+          for (int l = 0; l < L; ++l) o[l] = sq(n + l);
+          o[L] = sq(g);
+        }
+      }
+      break;
+    }
+    case MDP_SCN_TAG: {
+      for (int i = 0; i < n; ++i) {
+        if (!E.adversary[i]) continue;
+        float c = 0.f;
+        for (int a = 0; a < n; ++a)
+          if (!E.adversary[a] && dist2(p, a, i) < E.size[a] + E.size[i]) c += 1.f;
+        out[i * MDP_BENCH_W] = c;
+      }
+      break;
+    }
+    default:
+      break;
+  }
+}
+
 // World.step (core.py): action force, pairwise soft contact, damping,
 // integration with max_speed clamp.  p, v: [ne][2] of one env (in place).
 __device__ inline void env_physics(const EnvDesc& E, float* p, float* v, const float* act /*[n][5]*/) {
@@ -660,6 +719,7 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     env_physics(E, p, v, actv);
     float rew[MDP_MAX_AGENTS];
     env_reward(E, p, goal, rew);
+    if (a.bench) env_bench(E, p, goal, a.bench + (int64_t)(e0 + tid) * n * MDP_BENCH_W);
     for (int j = 0; j < n; ++j) {
       env_obs(E, p, v, goal, j, row + T.ag[j].nobs_off);
       row[T.ag[j].rew_off] = rew[j];

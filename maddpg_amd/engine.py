@@ -425,6 +425,16 @@ class Engine:
             self._keep = (a, uu)
             self.sync_out()
 
+    def env_step_bench(self, out=None):
+        """one vector env step (policy actions) that also returns every agent's
+        scenario benchmark_data() record, [E, n, BENCH_W] float32 on the device
+        (mdp_env_step_bench; --benchmark mode, train.py:139-141)."""
+        if out is None:
+            out = torch.empty((self.num_envs, self.n, _lib.BENCH_W), dtype=torch.float32, device=self.device)
+        self._c("mdp_env_step_bench", self._ptr(out))
+        self.sync_out()
+        return out
+
     def env_state(self):
         E, ne = self.num_envs, self.n_entities
         pos = np.empty((E, ne, 2), np.float32)

@@ -58,3 +58,18 @@ def spec(name, n_agents=None, num_adversaries=None):
         dims = [4 + 2 * L + 2 * (n - 1) + 2 * (ng if i < na else ng - 1) for i in range(n)]
         return ScenarioSpec(name, n, na, dims)
     raise ValueError(f"unknown scenario {name!r}")
+
+
+def bench_record(sp, row, i):
+    """Python value of agent i's scenario benchmark_data() (MPE returns tuples /
+    ints / floats; train.py:141 stores them in info_n['n']) from its device
+    record row (mdp_env_step_bench, MDP_BENCH_W floats)."""
+    if sp.name == "simple_spread":
+        return (float(row[0]), int(round(row[1])), float(row[2]), int(round(row[3])))
+    if sp.name == "simple_adversary":
+        if i < sp.num_adversaries:
+            return float(row[0])
+        return tuple(float(x) for x in row[:sp.n_agents])   # n-1 landmarks + goal
+    if sp.name == "simple_tag":
+        return int(round(row[0]))
+    raise AttributeError(f"scenario {sp.name!r} has no benchmark_data")

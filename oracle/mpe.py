@@ -103,6 +103,17 @@ class Scenario:
         d = self._dist(st["pos"][:, i], st["pos"][:, j])
         return d < (self.size[i] + self.size[j])
 
+    def benchmark_data(self, st):
+        """scenario.benchmark_data(agent, world) of every agent of the
+        post-physics state (environment._get_info, train.py:57-60,139-141):
+        a list over agents of per-env records [E, width]."""
+        raise AttributeError(f"scenario {self.name!r} has no benchmark_data")
+
+    def record(self, v, i):
+        """the Python value MPE's benchmark_data returns for agent i (tuple / int /
+        float) from its record row v (float array, MDP_BENCH_W wide)."""
+        raise AttributeError(f"scenario {self.name!r} has no benchmark_data")
+
 
 class Simple(Scenario):
     """scenarios/simple.py"""
@@ -184,6 +195,28 @@ class SimpleSpread(Scenario):
             rew[:, i] = r
         return rew
 
+    def benchmark_data(self, st):
+        """simple_spread.benchmark_data: (rew, collisions, min_dists, occupied_landmarks)."""
+        n = self.n_agents
+        p = st["pos"]
+        E = p.shape[0]
+        min_dists = np.zeros(E)
+        occupied = np.zeros(E)
+        for l in range(n):
+            m = np.stack([self._dist(p[:, a], p[:, n + l]) for a in range(n)], 1).min(1)
+            min_dists += m
+            occupied += (m < 0.1)
+        out = []
+        for i in range(n):
+            coll = np.zeros(E)
+            for a in range(n):                      # is_collision(a, agent) incl. self
+                coll += self.is_collision(st, a, i)
+            out.append(np.stack([-min_dists - coll, coll, min_dists, occupied], 1))
+        return out
+
+    def record(self, v, i):
+        return (float(v[0]), int(round(v[1])), float(v[2]), int(round(v[3])))
+
 
 class SimpleAdversary(Scenario):
     """scenarios/simple_adversary.py (1 adversary + 2 good, 2 landmarks)."""
@@ -243,6 +276,27 @@ class SimpleAdversary(Scenario):
             else:
                 rew[:, i] = pos_rew + adv_rew
         return rew
+
+    def benchmark_data(self, st):
+        """simple_adversary.benchmark_data: adversary |pos-goal|^2; good agents
+        (|pos-lm_l|^2 for every landmark, |pos-goal|^2)."""
+        n, L = self.n_agents, self.n_landmarks
+        p = st["pos"]
+        g = self._goal_pos(st)
+        out = []
+        for i in range(n):
+            if self.adversary[i]:
+                out.append(np.sum(np.square(p[:, i] - g), axis=1)[:, None])
+            else:
+                d = [np.sum(np.square(p[:, i] - p[:, n + l]), axis=1) for l in range(L)]
+                d.append(np.sum(np.square(p[:, i] - g), axis=1))
+                out.append(np.stack(d, 1))
+        return out
+
+    def record(self, v, i):
+        if self.adversary[i]:
+            return float(v[0])
+        return tuple(float(x) for x in v[:self.n_landmarks + 1])
 
 
 class SimpleTag(Scenario):
@@ -307,6 +361,23 @@ class SimpleTag(Scenario):
                     r -= b
                 rew[:, i] = r
         return rew
+
+    def benchmark_data(self, st):
+        """simple_tag.benchmark_data: adversary -> good agents in contact; good -> 0."""
+        n = self.n_agents
+        E = st["pos"].shape[0]
+        out = []
+        for i in range(n):
+            c = np.zeros(E)
+            if self.adversary[i]:
+                for a in range(n):
+                    if not self.adversary[a]:
+                        c += self.is_collision(st, a, i)
+            out.append(c[:, None])
+        return out
+
+    def record(self, v, i):
+        return int(round(v[0]))
 
 
 def make(name, **kw):

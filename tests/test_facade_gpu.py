@@ -143,3 +143,31 @@ def test_train_cli_runs(tmp_path, capsys, scenario, extra):
                      "--plots-dir", str(tmp_path) + "/", "--exp-name", "t2"] + extra)
     train(a2)
     assert "Loading previous state..." in capsys.readouterr().out
+
+
+@pytest.mark.parametrize("scenario,extra", [
+    ("simple_spread", []),
+    ("simple_tag", ["--num-adversaries", "3"]),
+    ("simple_adversary", ["--num-adversaries", "1"]),
+])
+def test_train_cli_benchmark_mode(tmp_path, capsys, scenario, extra):
+    """--benchmark (train.py:139-148): loads the saved policies, records
+    benchmark_data every step, pickles agent_info[:-1], trains nothing."""
+    import pickle
+    from experiments.train import parse_args, train
+    common = ["--scenario", scenario, "--batch-size", "64", "--max-episode-len", "5",
+              "--save-dir", str(tmp_path) + "/", "--plots-dir", str(tmp_path) + "/"] + extra
+    train(parse_args(common + ["--num-envs", "64", "--num-episodes", "100", "--save-rate", "50",
+                               "--exp-name", "t"]))
+    capsys.readouterr()
+    r = train(parse_args(common + ["--num-envs", "1", "--benchmark", "--benchmark-iters", "12",
+                                   "--benchmark-dir", str(tmp_path) + "/bench/", "--exp-name", "b"]))
+    out = capsys.readouterr().out
+    assert "Loading previous state..." in out and "Finished benchmarking, now saving..." in out
+    assert r.rounds == 0
+    info = pickle.load(open(str(tmp_path) + "/bench/b.pkl", "rb"))
+    # E=1, 5-step episodes, stop at the first terminal with train_step > 12 (t=15):
+    # entries = episodes 1..3 closed; first holds 4 steps, then 5 each
+    assert [len(ep[0]) for ep in info] == [4, 5, 5]
+    assert all(len(ep) == 1 for ep in info)
+    assert all(len(step) == r.n for ep in info for step in ep[0])

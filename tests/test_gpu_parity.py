@@ -385,3 +385,34 @@ def test_full_size_index_stream_properties():
         want = [g.randint(0, 999_999) for _ in range(6 * 4096)]
         np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(eng.get_rng_state(), np.array(g.getstate()[1], np.uint32))
+
+
+# ------------------------------------------------------- --benchmark records
+@pytest.mark.parametrize("name,n,na", [s for s in SCENARIOS if s[0] != "simple"])
+def test_env_benchmark_data_parity(name, n, na):
+    """mdp_env_step_bench: every agent's benchmark_data() record of the
+    post-physics state equals the oracle's on that same (device) state."""
+    from maddpg_amd.envs import bench_record, spec
+    sp = spec(name, n, na if na else None)
+    E = 37
+    eng = Engine(sp.obs_dims, batch_size=16, capacity=1000, num_envs=E, scenario=name,
+                 num_adversaries=sp.num_adversaries, max_episode_len=25, seed=5)
+    eng.init_params(2)
+    eng.env_reset()
+    sc = _oracle_scn(name, n, na)
+    for _ in range(4):
+        info = eng.env_step_bench().cpu().numpy()
+        st = eng.env_state()                       # not terminal: the post-physics state
+        ost = {"pos": st["pos"].astype(np.float64), "vel": st["vel"].astype(np.float64), "goal": st["goal"]}
+        want = sc.benchmark_data(ost)
+        for i in range(n):
+            w = want[i]
+            np.testing.assert_allclose(info[:, i, :w.shape[1]], w, rtol=1e-5, atol=2e-5)
+            assert np.all(info[:, i, w.shape[1]:] == 0)
+            for e in range(0, E, 7):
+                got_rec, want_rec = bench_record(sp, info[e, i], i), sc.record(w[e], i)
+                assert type(got_rec) is type(want_rec)
+    # simple has no benchmark_data (the reference's make_env raises)
+    s1 = Engine([4], batch_size=16, capacity=100, num_envs=4, scenario="simple")
+    with pytest.raises(Exception, match="benchmark_data"):
+        s1.env_step_bench()

@@ -89,3 +89,71 @@ def test_product_path_refuses_without_gpu():
     from maddpg_amd.engine import Engine
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         Engine([4], batch_size=8, capacity=16)
+
+
+class _StubEngine:
+    """CPU stand-in for Engine.env_step_bench (host logic only): the oracle's
+    spread records of a random state each step."""
+
+    def __init__(self, E, n):
+        import numpy as np
+        from oracle import mpe
+        self.rng = np.random.default_rng(0)
+        self.sc = mpe.SimpleSpread(n)
+        self.E, self.n = E, n
+
+    def env_step_bench(self):
+        import numpy as np
+        import torch
+        st = self.sc.reset(self.rng, self.E)
+        recs = self.sc.benchmark_data(st)
+        out = np.zeros((self.E, self.n, 8), np.float32)
+        for i in range(self.n):
+            out[:, i, :recs[i].shape[1]] = recs[i]
+        return torch.from_numpy(out)
+
+
+def test_benchmark_mode_pickle_structure(tmp_path):
+    """train.py:139-148 agent_info bookkeeping with E env copies (stub engine)."""
+    import pickle
+    import types
+    from experiments.train import benchmark, parse_args
+    from maddpg_amd.envs import spec
+    for E, iters, want in [(1, 12, [4, 5, 5]), (2, 12, [4, 4, 5, 5]), (1, 0, [4])]:
+        a = parse_args(["--scenario", "simple_spread", "--max-episode-len", "5", "--num-envs", str(E),
+                        "--benchmark-iters", str(iters), "--benchmark-dir", str(tmp_path) + "/"])
+        runner = types.SimpleNamespace(eng=_StubEngine(E, 3), spec=spec("simple_spread"), n=3,
+                                       synchronize=lambda: None)
+        benchmark(a, runner, "x", 0)
+        info = pickle.load(open(str(tmp_path) + "/x.pkl", "rb"))
+        assert [len(ep[0]) for ep in info] == want
+        rec = info[0][0][0][0]
+        assert isinstance(rec, tuple) and len(rec) == 4 and isinstance(rec[1], int) and rec[1] >= 1
+        assert abs(rec[0] - (-rec[2] - rec[1])) < 1e-4
+
+
+def test_oracle_benchmark_records():
+    import numpy as np
+    from maddpg_amd.envs import bench_record, spec
+    from oracle import mpe
+    rng = np.random.default_rng(1)
+    for name, sc, sp in [("simple_spread", mpe.SimpleSpread(3), spec("simple_spread")),
+                         ("simple_adversary", mpe.SimpleAdversary(), spec("simple_adversary")),
+                         ("simple_tag", mpe.SimpleTag(), spec("simple_tag"))]:
+        st = sc.reset(rng, 50)
+        recs = sc.benchmark_data(st)
+        assert len(recs) == sc.n_agents
+        for i, r in enumerate(recs):
+            row = np.zeros(8, np.float32)
+            row[:r.shape[1]] = r[0]
+            a, b = bench_record(sp, row, i), sc.record(r[0], i)
+            assert type(a) is type(b)
+            if isinstance(a, tuple):
+                np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
+            else:
+                assert abs(a - b) < 1e-5
+    try:
+        mpe.Simple().benchmark_data(mpe.Simple().reset(rng, 1))
+        raise AssertionError("simple has no benchmark_data")
+    except AttributeError:
+        pass
