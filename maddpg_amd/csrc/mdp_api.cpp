@@ -273,8 +273,6 @@ struct mdp_handle {
   bool general_grads = false;
   // single-GPU optimizer step as one k_reduce_apply launch (MDP_UNFUSED_APPLY=1: k_reduce + k_apply)
   bool fused_apply = true;
-  bool merge = true;      // merged optimizer steps in the round paths (MDP_NO_MERGE=1: off)
-  int pending_ra = -1;    // agent whose actor step is still to be launched (merged rounds)
   uint32_t* ra_ctr = nullptr;
   double* ra_part = nullptr;
   hipGraph_t round_graph = nullptr;
@@ -388,18 +386,8 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
   return 0;
 }
 
-MergeArgs no_merge(mdp_handle* h) {
-  MergeArgs m;
-  memset(&m, 0, sizeof(m));
-  m.wait_agent = -1;
-  m.ctl = h->ctl;
-  return m;
-}
-
-int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr,
-                   const MergeArgs* mg = nullptr) {
+int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr) {
   CriticArgs a;
-  a.mg = mg ? *mg : no_merge(h);
   a.pf_ctl = h->ctl;
   a.pf_out = nullptr;
   a.pf_count = 0;
@@ -420,8 +408,6 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.slab_stat = h->stat_c;
   a.y_out = h->y;
   ProfScope p(h, MDP_K_CRITIC_GRAD);
-  if (a.mg.nra && (h->general_grads || !grads_r_ok(h->L.topo, agent)))
-    return fail(h, "merged optimizer step needs the fast critic kernel");
   if (!h->general_grads && grads_r_ok(h->L.topo, agent)) {
     if (pf_out) {
       a.pf_out = pf_out;
@@ -440,9 +426,8 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   return 0;
 }
 
-int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, const MergeArgs* mg = nullptr) {
+int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act) {
   ActorArgs a;
-  a.mg = mg ? *mg : no_merge(h);
   a.topo = h->L.topo;
   a.agent = agent;
   a.B = h->cfg.batch_size;
@@ -458,8 +443,6 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
   a.slab_stride = h->L.slab_a;
   a.slab_stat = h->stat_a;
   ProfScope p(h, MDP_K_ACTOR_GRAD);
-  if (a.mg.nra && (h->general_grads || !grads_r_ok(h->L.topo, agent)))
-    return fail(h, "merged optimizer step needs the fast actor kernel");
   if (!h->general_grads && grads_r_ok(h->L.topo, agent)) {
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
     return 0;
@@ -529,7 +512,7 @@ bool reduce_apply_ok(const mdp_handle* h, int agent, int net) {
   return true;
 }
 
-FusedApplyArgs fused_args(mdp_handle* h, int agent, int net) {
+int do_reduce_apply(mdp_handle* h, int agent, int net) {
   FusedApplyArgs f;
   f.ap = apply_args(h, agent, net, 1.0f);
   f.ap.slab = net ? h->slab_c : h->slab_a;
@@ -540,35 +523,9 @@ FusedApplyArgs fused_args(mdp_handle* h, int agent, int net) {
   f.sync_ctr = h->ra_ctr + (int64_t)g * 8 * 32;
   f.done_ctr = f.sync_ctr + 6 * 32;
   f.sync_part = h->ra_part + (int64_t)g * 6 * MDP_RA_MAXCH;
-  static const int ra_dbg = getenv("MDP_RA_DBG") ? atoi(getenv("MDP_RA_DBG")) : 0;
-  f.dbg = ra_dbg;
-  return f;
-}
-
-int do_reduce_apply(mdp_handle* h, int agent, int net, bool bump = true) {
-  FusedApplyArgs f = fused_args(h, agent, net);
-  if (!bump) f.ap.bump_ctr = 0;
   ProfScope p(h, MDP_K_REDUCE_APPLY);
   HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
   return 0;
-}
-
-// the optimizer step of (agent, net) as the leading workgroups of the next
-// gradient launch (MergeArgs, mdp_kernels.h).  The noise-counter bump moves
-// from the actor step to the grid end of the actor-gradient launch.
-MergeArgs merge_args(mdp_handle* h, int agent, int net, int wait_agent, int bump) {
-  MergeArgs m = no_merge(h);
-  m.ra = fused_args(h, agent, net);
-  m.ra.ap.bump_ctr = 0;
-  const ApplyArgs& a = m.ra.ap;
-  m.nra = m.ra.rblk[6] + (a.polyak ? a.oblk[6] : 0) + (a.stats_mode ? 1 : 0);
-  m.pub = net ? 1 : 2;
-  m.ready = m.ra.done_ctr + 32;  // counter 7 of the (agent, net) sync block
-  m.seq_slot = agent * 2 + net;
-  m.nch = m.ra.rblk[6];
-  m.wait_agent = wait_agent;
-  m.bump_ctr = bump;
-  return m;
 }
 
 int do_reduce(mdp_handle* h, int agent, int net) {
@@ -667,37 +624,6 @@ int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, 
   return 0;
 }
 
-// merged rounds: is agent's update eligible (single GPU, fast kernels, fused optimizer steps)?
-bool merge_ok(const mdp_handle* h, int agent) {
-  return h->merge && !h->comm && h->fused_apply && !h->general_grads && grads_r_ok(h->L.topo, agent) &&
-         reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
-}
-
-// launch the actor step a merged update left pending (standalone; no noise bump)
-int flush_pending(mdp_handle* h) {
-  if (h->pending_ra < 0) return 0;
-  const int ag = h->pending_ra;
-  h->pending_ra = -1;
-  return do_reduce_apply(h, ag, 0, false);
-}
-
-// one agent's update in a merged round: critic kernel (+ the pending actor step
-// of the previous update), actor kernel (+ this critic step); this actor step
-// stays pending for the next launch
-int do_update_merged(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out) {
-  MergeArgs mc = no_merge(h);
-  if (h->pending_ra >= 0) {
-    mc = merge_args(h, h->pending_ra, 0, h->pending_ra, 0);
-    h->pending_ra = -1;
-  }
-  int rc = do_critic_grad(h, agent, idx, nullptr, pf_out, &mc);
-  if (rc) return rc;
-  const MergeArgs ma = merge_args(h, agent, 1, -1, 1);
-  if ((rc = do_actor_grad(h, agent, idx, nullptr, &ma))) return rc;
-  h->pending_ra = agent;
-  return 0;
-}
-
 int set_ring(mdp_handle* h, int64_t len, int64_t next) {
   h->len = len;
   h->next = next;
@@ -736,8 +662,6 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->general_grads = g && g[0] == '1';
     const char* u = getenv("MDP_UNFUSED_APPLY");
     h->fused_apply = !(u && u[0] == '1');
-    const char* nm = getenv("MDP_NO_MERGE");
-    h->merge = !(nm && nm[0] == '1');
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
@@ -1063,20 +987,10 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
   return do_update(h, agent, idx, u_tgt_dev, u_act_dev);
 }
 
-// one round (every agent in order); merged updates may leave the last actor
-// step pending -- the caller flushes (flush_pending) before its sequence ends
 static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nullptr) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   int rc = 0;
-  for (int i = 0; i < n && !rc; ++i) {
-    int32_t* pf = i == 0 ? pf_out : nullptr;
-    if (merge_ok(h, i)) {
-      rc = do_update_merged(h, i, idx + (int64_t)i * B, pf);
-    } else {
-      rc = flush_pending(h);
-      if (!rc) rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, pf);
-    }
-  }
+  for (int i = 0; i < n && !rc; ++i) rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, i == 0 ? pf_out : nullptr);
   return rc;
 }
 
@@ -1089,9 +1003,7 @@ static int round_launches(mdp_handle* h) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   int rc = launch_make_index(h, n * B, h->index);
   if (rc) return rc;
-  rc = round_updates(h, h->index);
-  const int rf = flush_pending(h);
-  return rc ? rc : rf;
+  return round_updates(h, h->index);
 }
 
 static bool any_prof(const mdp_handle* h) {
@@ -1298,13 +1210,9 @@ static int step_launches(mdp_handle* h, int rounds) {
   for (int r = 0; r < rounds && !rc; ++r) {
     const bool more = r + 1 < rounds;
     rc = round_updates(h, slot[r & 1], (more && pf) ? slot[(r + 1) & 1] : nullptr);
-    if (!rc && more && !pf) {
-      rc = flush_pending(h);  // the index kernel is no gradient launch to merge into
-      if (!rc) rc = launch_make_index(h, nb, slot[(r + 1) & 1]);
-    }
+    if (!rc && more && !pf) rc = launch_make_index(h, nb, slot[(r + 1) & 1]);
   }
-  const int rf = flush_pending(h);
-  return rc ? rc : rf;
+  return rc;
 }
 
 int mdp_train_step(mdp_handle* h, int32_t rounds) {

@@ -21,10 +21,179 @@
 // AdamOptimizer._finish update) and, for the actor step, the noise counter.
 #include "mdp_device.h"
 #include "mdp_kernels.h"
-#include "mdp_ra.h"
+
+namespace {
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+__device__ __forceinline__ void st_agent(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace
 
 __global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
-  ra_block<1024>(f, blockIdx.x, gridDim.x, 0, nullptr);
+  const ApplyArgs& a = f.ap;
+  __shared__ f32x4 red[16][64];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (b < f.rblk[6]) {
+    int t = 0;
+    while (b >= f.rblk[t + 1]) ++t;
+    const TDesc td = a.net.t[t];
+    const int n = td.rows * td.cols;
+    const int nch = f.rblk[t + 1] - f.rblk[t];
+    const int c = b - f.rblk[t];
+    const int col = tid & 63, grp = tid >> 6;
+    const int p0 = c * MDP_RA_CHUNK + 4 * col;  // this thread's 4 parameters (tensor-relative)
+    const bool act = p0 < n;
+    const int64_t i0 = td.off + p0;             // absolute parameter index
+    // Adam state of the chunk, requested with the partial-gradient loads
+    f32x4 m4 = {0.f, 0.f, 0.f, 0.f}, v4 = m4, th4 = m4, tg4 = m4;
+    const float b1p = a.beta[0], b2p = a.beta[1];  // this step's powers (advanced at the end)
+    if (grp == 0 && act) {
+      m4 = ld4(a.m + i0);
+      v4 = ld4(a.v + i0);
+      th4 = ld4(a.theta + i0);
+      if (a.polyak) tg4 = ld4(a.target + i0);
+    }
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (act) {
+      const float* base = a.slab + (td.off - a.net.off) + p0;
+      f32x4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int w = grp + 16 * k;
+        v[k] = w < a.nwg ? ld4(base + (int64_t)w * a.slab_stride) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      s = ((v[0] + v[1]) + v[2]) + v[3];
+      for (int w = grp + 64; w < a.nwg; w += 16) s += ld4(base + (int64_t)w * a.slab_stride);
+    }
+    red[grp][col] = s;
+    __syncthreads();
+    if (grp == 0) {
+      f32x4 g = red[0][col];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) g += red[q][col];
+      double ss = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gs = g[j] * a.scale;
+        if (p0 + j < n) ss += (double)gs * (double)gs;
+      }
+      ss = wave_sum_d(ss);
+      if (act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (p0 + j < n) a.grad[i0 + j] = g[j];
+      }
+      double tot = ss;
+      if (nch > 1) {
+        double* part = f.sync_part + t * MDP_RA_MAXCH;
+        uint32_t* ctr = f.sync_ctr + t * 32;
+        if (lane == 0) {
+          st_agent(part + c, ss);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t target = (prev / (uint32_t)nch + 1u) * (uint32_t)nch;
+          uint32_t it = 0;
+          while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++it > kSpinLimit) {
+              __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        tot = 0.0;
+        for (int q = lane; q < nch; q += 64) tot += ld_agent(part + q);
+        tot = wave_sum_d(tot);
+      }
+      if (act) {
+        const float norm = (float)sqrt(tot);
+        const float clip = a.clip;
+        const float denom = fmaxf(norm, clip);
+        const float one = 1.0f;
+        const float alpha = a.lr * sqrtf(one - b2p) / (one - b1p);
+        const float c1 = one - a.b1, c2 = one - a.b2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (p0 + j < n) {
+            const float gc = ((g[j] * a.scale) * clip) / denom;
+            const float m = m4[j] + (gc - m4[j]) * c1;
+            const float v = v4[j] + (gc * gc - v4[j]) * c2;
+            const float th = th4[j] - (m * alpha) / (sqrtf(v) + a.eps);
+            a.m[i0 + j] = m;
+            a.v[i0 + j] = v;
+            a.theta[i0 + j] = th;
+            if (a.polyak) a.target[i0 + j] = a.pa * tg4[j] + a.pb * th;
+          }
+        }
+      }
+    }
+  } else if (a.polyak && b < f.rblk[6] + a.oblk[6]) {
+    const int bb = b - f.rblk[6];
+    int t = 0;
+    while (bb >= a.oblk[t + 1]) ++t;
+    const TDesc td = a.other.t[t];
+    const int n = td.rows * td.cols;
+    const int e0 = (bb - a.oblk[t]) * MDP_APPLY_CHUNK;
+    const int e1 = min(n, e0 + MDP_APPLY_CHUNK);
+    for (int e = e0 + tid; e < e1; e += blockDim.x) {
+      const int64_t i = td.off + e;
+      a.target[i] = a.pa * a.target[i] + a.pb * a.theta[i];
+    }
+  } else if (a.stats_mode && tid < 64) {
+    // stats workgroup (maddpg.py:196), as in k_apply
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int w = tid; w < a.nwg; w += 64) {
+      const double* st = a.slab_stat + (int64_t)w * 8;
+      s0 += st[0];
+      s1 += st[1];
+      s2 += st[2];
+      s3 += st[3];
+    }
+    s0 = wave_sum_d(s0);
+    s1 = wave_sum_d(s1);
+    if (a.stats_mode == 1) {
+      s2 = wave_sum_d(s2);
+      s3 = wave_sum_d(s3);
+      const double mean_y = s1 / a.B;
+      double dv = 0.0;
+      for (int i = tid; i < a.B; i += 64) {
+        const double d = a.y[i] - mean_y;
+        dv += d * d;
+      }
+      dv = wave_sum_d(dv);
+      if (tid == 0) {
+        a.stats_out[0] = s0 / a.B;
+        a.stats_out[2] = mean_y;
+        a.stats_out[3] = s2 / a.B;
+        a.stats_out[4] = s3 / a.B;
+        a.stats_out[5] = sqrt(dv / a.B);
+      }
+    } else if (tid == 0) {
+      a.stats_out[1] = -s0 / a.B + (double)a.reg * (s1 / ((double)a.B * MDP_ACT_DIM));
+    }
+  }
+  // the last workgroup to finish advances the optimizer step (every net
+  // workgroup read beta before its add, so nobody reads the new values here)
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t nb = gridDim.x;
+    const uint32_t prev = __hip_atomic_fetch_add(f.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev % nb == nb - 1) {
+      const float p1 = a.beta[0], p2 = a.beta[1];
+      a.beta[2] = p1;
+      a.beta[3] = p2;
+      a.beta[0] = p1 * a.b1;
+      a.beta[1] = p2 * a.b2;
+      if (a.bump_ctr) a.ctl->upd_ctr += 1u;
+    }
+  }
 }
 
 hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {

@@ -654,57 +654,8 @@ struct LdsCarve {
 
 __device__ __forceinline__ f32x4 ld4(const float* __restrict__ p) { return *reinterpret_cast<const f32x4*>(p); }
 
-// ---- write-through hand-off inside one launch (MI355X_MICROARCH.md "Valid forms",
-// row 1): the producer stores every handed-off byte sc1 and drains, one lane adds
-// to an agent-scope counter; the consumer wave polls that counter with sc1 loads
-// and then reads EVERY handed-off byte with buffer loads carrying sc1 (they bypass
-// the CU's L1, so no acquire fence).  `base` must be wave-uniform.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t mdp_rsrc(const float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
-}
-template <bool SC1>
-__device__ __forceinline__ f32x4 ldw4(const float* __restrict__ base, int e) {
-  if constexpr (SC1) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(mdp_rsrc(base), e * 4, 0, 16));
-  } else {
-    return ld4(base + e);
-  }
-}
-template <bool SC1>
-__device__ __forceinline__ float ldw1(const float* __restrict__ base, int e) {
-  if constexpr (SC1) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mdp_rsrc(base), e * 4, 0, 16));
-  } else {
-    return base[e];
-  }
-}
-__device__ __forceinline__ void stw4_sc1(float* base, int e, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                         mdp_rsrc(base), e * 4, 0, 16);
-}
-__device__ __forceinline__ void stw1_sc1(float* base, int e, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), mdp_rsrc(base), e * 4, 0, 16);
-}
-typedef __attribute__((address_space(1))) uint32_t mdp_gu32;
-// one lane of the calling wave polls *ctr (sc1) until it reaches `target`
-// (wrap-safe); bounded: on timeout sets *fault and returns.  Wave-uniform exit.
-__device__ __forceinline__ void mdp_wait_count(const uint32_t* ctr, uint32_t target, uint32_t* fault) {
-  if ((threadIdx.x & 63) == 0) {
-    uint32_t it = 0;
-    while ((int32_t)(__hip_atomic_load((mdp_gu32*)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++it > (1u << 22)) {
-        __hip_atomic_store((mdp_gu32*)fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
-}
-
 // w[s] = W[4s+kq][4r .. 4r+3] of W[K][64]; rows >= K or inside [mlo, mhi) read as zero
-template <int KS, bool SC1 = false>
+template <int KS>
 __device__ __forceinline__ void rf_load(f32x4 (&w)[KS], const float* __restrict__ W, int K, int mlo, int mhi) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
 #pragma unroll
@@ -712,7 +663,7 @@ __device__ __forceinline__ void rf_load(f32x4 (&w)[KS], const float* __restrict_
     w[s] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (4 * s < K) {
       const int k = 4 * s + kq;
-      const f32x4 v = ldw4<SC1>(W, min(k, K - 1) * MDP_RH + 4 * r);
+      const f32x4 v = ld4(W + min(k, K - 1) * MDP_RH + 4 * r);
       const bool z = k >= K || (k >= mlo && k < mhi);
       w[s] = f32x4{z ? 0.f : v[0], z ? 0.f : v[1], z ? 0.f : v[2], z ? 0.f : v[3]};
     }
@@ -757,13 +708,12 @@ __device__ __forceinline__ void rf_store(const f32x4 (&acc)[4], f32x4 b, float* 
 }
 
 // output head with nout <= 16 columns on one MFMA tile (column r), K = 64
-template <bool SC1 = false>
 __device__ __forceinline__ void rh_load(float (&w)[16], const float* __restrict__ W, int nout) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int c = min(r, nout - 1);
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    const float v = ldw1<SC1>(W, (4 * s + kq) * nout + c);
+    const float v = W[(4 * s + kq) * nout + c];
     w[s] = r < nout ? v : 0.f;
   }
 }
@@ -780,11 +730,10 @@ __device__ __forceinline__ f32x4 rh_acc(const float* X, int ldx, const float (&w
 }
 
 // scalar head (nout = 1) on the VALU: lane (row = lane >> 2, q = lane & 3), w[j] = W3[4j + q]
-template <bool SC1 = false>
 __device__ __forceinline__ void rq_load(float (&w)[16], const float* __restrict__ W) {
   const int q = threadIdx.x & 3;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) w[j] = ldw1<SC1>(W, 4 * j + q);
+  for (int j = 0; j < 16; ++j) w[j] = W[4 * j + q];
 }
 // returns sum_k X[row][k] W3[k] in all 4 lanes of the row
 __device__ __forceinline__ float rq_head(const float* X, int ldx, const float (&w)[16]) {
@@ -825,12 +774,11 @@ __device__ __forceinline__ void rt_acc(f32x4& acc, const float* X, int ldx, int 
 // transposed tile for dX = dY @ W^T (W[K][64] row-major): output column kk = W row,
 // contraction n = 16 kq + s, so a lane's 16 fragments are one contiguous 64-B run
 // of row kk: w[m] = W[kk][16 kq + 4m .. +3]; ok = false zeroes the fragment
-template <bool SC1 = false>
 __device__ __forceinline__ void rdg_load(f32x4 (&w)[4], const float* __restrict__ W, int kk, bool ok) {
   const int kq = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
-    const f32x4 v = ldw4<SC1>(W, kk * MDP_RH + 16 * kq + 4 * m);
+    const f32x4 v = ld4(W + kk * MDP_RH + 16 * kq + 4 * m);
     w[m] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 }

@@ -33,7 +33,6 @@
 #include "mdp_device.h"
 #include "mdp_kernels.h"
 #include "mdp_mt.h"
-#include "mdp_ra.h"
 
 namespace {
 constexpr int RH = MDP_RH, LH = MDP_RLH, LD = MDP_RLD;
@@ -58,40 +57,15 @@ __device__ __forceinline__ void dgrad_tile(const float* dY, const f32x4 (&w)[4],
     dX[row * LD + col] = Hin[row * LH + col] > 0.f ? acc[i] : 0.f;
   }
 }
-// end of a workgroup of a merged launch: the grid-last workgroup advances the
-// hand-off sequence (and the training-noise counter); every workgroup read both
-// at its start, before any workgroup could be last
-__device__ __forceinline__ void merged_grid_end(const MergeArgs& mg) {
-  if (mg.nra == 0 && !mg.bump_ctr) return;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t* tk = &mg.ctl->ticket[4];
-    const uint32_t prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      if (mg.nra) mg.ctl->ho_seq[mg.seq_slot] += 1u;
-      if (mg.bump_ctr) mg.ctl->upd_ctr += 1u;
-      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
 }  // namespace
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
-  const MergeArgs& mg = a.mg;
-  if ((int)blockIdx.x < mg.nra) {  // the previous actor step (merged launch)
-    ra_block<512>(mg.ra, blockIdx.x, mg.nra, mg.pub, mg.ready);
-    merged_grid_end(mg);
-    return;
-  }
-  const int bx = blockIdx.x - mg.nra;
-  if (a.pf_count > 0 && (int)blockIdx.x == (int)gridDim.x - 1) {
+  if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
     // the next round's index draw (same ring length, the MT stream continues):
     // one workgroup beside the B/16 of this kernel, so it costs no time of its own
     make_index_block<512>(a.pf_ctl, a.pf_count, a.pf_out);
-    merged_grid_end(mg);
     return;
   }
-  const uint32_t ho_target = mg.nra ? (mg.ctl->ho_seq[mg.seq_slot] + 1u) * (uint32_t)mg.nch : 0u;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;  // gather waves done (LDS hand-off, replaces a barrier)
   const Topo& T = a.topo;
@@ -124,12 +98,12 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const int r0 = bx * MDP_R;
+  const int r0 = blockIdx.x * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const uint32_t ctr = a.ctl->upd_ctr;
   const float* Pc = a.theta;
   const float* Pt = a.target;
-  float* slab = a.slab + (int64_t)bx * a.slab_stride - nd.off;
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
   MDP_STAMP(0);
   if (threadIdx.x == 0) rows_ready = 0;
   __syncthreads();  // B0 (nothing in flight yet)
@@ -152,26 +126,11 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 #endif
       f32x4 w1[16], w2[16];
       float w3[16];
-      f32x4 b1, b2;
-      float b3;
-      if (j == mg.wait_agent) {
-        // this target actor was Polyak-updated by the merged actor step: wait for
-        // its chunks, then read it write-through (sc1)
-        mdp_wait_count(mg.ready, ho_target, &mg.ctl->fault);
-        rf_load<16, true>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
-        rf_load<16, true>(w2, Pt + an.t[2].off, RH, 0, 0);
-        rh_load<true>(w3, Pt + an.t[4].off, MDP_ACT_DIM);
-        b1 = ldw4<true>(Pt + an.t[1].off, 4 * r);
-        b2 = ldw4<true>(Pt + an.t[3].off, 4 * r);
-        b3 = ldw1<true>(Pt + an.t[5].off, min(r, MDP_ACT_DIM - 1));
-      } else {
-        rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
-        rf_load<16>(w2, Pt + an.t[2].off, RH, 0, 0);
-        rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
-        b1 = ld4(Pt + an.t[1].off + 4 * r);
-        b2 = ld4(Pt + an.t[3].off + 4 * r);
-        b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
-      }
+      rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
+      rf_load<16>(w2, Pt + an.t[2].off, RH, 0, 0);
+      rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
+      const f32x4 b1 = ld4(Pt + an.t[1].off + 4 * r), b2 = ld4(Pt + an.t[3].off + 4 * r);
+      const float b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
       // Gumbel noise of the target action, computed while the weights are in flight
       float gn[MDP_ACT_DIM];
       {
@@ -340,7 +299,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       s_r = sum16(s_r);
       s_q = sum16(s_q);
       if (lane == 0) {
-        double* st = a.slab_stat + (int64_t)bx * 8;
+        double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
         st[0] = s_l;
         st[1] = s_y;
         st[2] = s_r;
@@ -373,17 +332,9 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   if (kb_c) wgrad_waves(rowbuf + ag.act_off, ldr, kb_c, d1, LD, RH, slab + nd.t[0].off + ka_c * RH, 0, 8);
   if (wave == 7) colsum64(d1, LD, slab + nd.t[1].off);
   MDP_STAMP(10);
-  merged_grid_end(mg);
 }
 
 __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
-  const MergeArgs& mg = a.mg;
-  if ((int)blockIdx.x < mg.nra) {  // this agent's critic step (merged launch)
-    ra_block<512>(mg.ra, blockIdx.x, mg.nra, mg.pub, mg.ready);
-    merged_grid_end(mg);
-    return;
-  }
-  const int bx = blockIdx.x - mg.nra;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;
   const Topo& T = a.topo;
@@ -412,14 +363,11 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const int r0 = bx * MDP_R;
+  const int r0 = blockIdx.x * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const uint32_t ctr = a.ctl->upd_ctr;
   const float* P = a.theta;
-  float* slab = a.slab + (int64_t)bx * a.slab_stride - na.off;
-  // merged critic step: the critic (theta) is published by the leading workgroups
-  const bool ho = mg.nra > 0;
-  const uint32_t ho_target = ho ? (mg.ctl->ho_seq[mg.seq_slot] + 1u) * (uint32_t)mg.nch : 0u;
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
   MDP_STAMP(16);
   if (threadIdx.x == 0) rows_ready = 0;
   __syncthreads();  // B0
@@ -471,12 +419,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       wave_sync();
       if (lane < MDP_R) gumbel_softmax5_pre(lg + lane * 8, gn, av + lane * 8);
       // backward-phase weights: W1c rows of the a_i input (for da) and W3 of the actor (for d2a)
-      if (ho) {
-        mdp_wait_count(mg.ready, ho_target, &mg.ctl->fault);
-        rdg_load<true>(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
-      } else {
-        rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
-      }
+      rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
 #pragma unroll
       for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
       MDP_STAMP(18);
@@ -513,7 +456,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       s_q = sum16(s_q);
       s_p = sum16(s_p);
       if (lane == 0) {
-        double* st = a.slab_stat + (int64_t)bx * 8;
+        double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
         st[0] = s_q;
         st[1] = s_p;
       }
@@ -546,28 +489,13 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       // ---------------- critic (post-step weights) forward with a_i = the sample (maddpg.py:48-52)
       f32x4 w1[20], w1b[2], w2[16];
       float w3[16];
-      f32x4 b1, b2;
-      float b3, w3c;
-      if (ho) {  // the critic just stepped in this launch: wait, then read it write-through
-        mdp_wait_count(mg.ready, ho_target, &mg.ctl->fault);
-        rf_load<20, true>(w1, P + nc.t[0].off, ka_c, ag.a_in_off, ag.a_in_off + MDP_ACT_DIM);
-        rf_load<2, true>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM, 0, 0);
-        rf_load<16, true>(w2, P + nc.t[2].off, RH, 0, 0);
-        rq_load<true>(w3, P + nc.t[4].off);
-        b1 = ldw4<true>(P + nc.t[1].off, 4 * r);
-        b2 = ldw4<true>(P + nc.t[3].off, 4 * r);
-        b3 = ldw1<true>(P + nc.t[5].off, 0);
-        w3c = ldw1<true>(P + nc.t[4].off, lane);
-      } else {
-        rf_load<20>(w1, P + nc.t[0].off, ka_c, ag.a_in_off, ag.a_in_off + MDP_ACT_DIM);
-        rf_load<2>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM, 0, 0);
-        rf_load<16>(w2, P + nc.t[2].off, RH, 0, 0);
-        rq_load(w3, P + nc.t[4].off);
-        b1 = ld4(P + nc.t[1].off + 4 * r);
-        b2 = ld4(P + nc.t[3].off + 4 * r);
-        b3 = P[nc.t[5].off];
-        w3c = P[nc.t[4].off + lane];
-      }
+      rf_load<20>(w1, P + nc.t[0].off, ka_c, ag.a_in_off, ag.a_in_off + MDP_ACT_DIM);
+      rf_load<2>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM, 0, 0);
+      rf_load<16>(w2, P + nc.t[2].off, RH, 0, 0);
+      rq_load(w3, P + nc.t[4].off);
+      const f32x4 b1 = ld4(P + nc.t[1].off + 4 * r), b2 = ld4(P + nc.t[3].off + 4 * r);
+      const float b3 = P[nc.t[5].off];
+      const float w3c = P[nc.t[4].off + lane];
       lds_wait(&rows_ready, 6);
       f32x4 acc[4];
       rf_zero(acc);
@@ -610,13 +538,8 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 128, 384);
     lds_signal(&rows_ready);
     f32x4 wc[4], wa[4];
+    rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);
     rdg_load(wa, P + na.t[2].off, 16 * tt + r, true);
-    if (ho) {
-      mdp_wait_count(mg.ready, ho_target, &mg.ctl->fault);
-      rdg_load<true>(wc, P + nc.t[2].off, 16 * tt + r, true);
-    } else {
-      rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);
-    }
     __syncthreads();  // B2
     __syncthreads();  // B3
     if (tt == 0) MDP_STAMPW(21);
@@ -633,7 +556,6 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   wgrad_waves(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1a, LD, RH, slab + na.t[0].off, 0, 8);
   if (wave == 7) colsum64(d1a, LD, slab + na.t[1].off);
   MDP_STAMP(27);
-  merged_grid_end(mg);
 }
 
 namespace {
@@ -644,7 +566,7 @@ hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr, int 
     (void)hipGetLastError();
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(a.mg.nra + (a.B + MDP_R - 1) / MDP_R + extra), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(kern, dim3((a.B + MDP_R - 1) / MDP_R + extra), dim3(512), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace

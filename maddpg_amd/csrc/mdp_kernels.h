@@ -5,6 +5,46 @@
 
 #include "mdp_topo.h"
 
+struct CriticArgs {
+  Topo topo;
+  int agent, B;
+  const float* theta;
+  const float* target;
+  const float* replay;
+  const int32_t* idx;
+  const float* u_tgt;   // [n][B][5] or null
+  uint64_t seed;
+  const Ctl* ctl;
+  double gamma;
+  float inv_b;
+  float* slab;          // [nwg][slab_stride] partial critic grads (net-relative)
+  int slab_stride;
+  double* slab_stat;    // [nwg][8]
+  double* y_out;        // [B]
+  int group;            // target actors run concurrently per pass (LDS budget)
+  // k_critic_grad_r only: one extra workgroup draws the NEXT round's indices
+  // (pf_count draws into pf_out) while this kernel runs (0: none)
+  Ctl* pf_ctl;
+  int32_t* pf_out;
+  int pf_count;
+};
+
+struct ActorArgs {
+  Topo topo;
+  int agent, B;
+  const float* theta;
+  const float* replay;
+  const int32_t* idx;
+  const float* u_act;   // [B][5] or null
+  uint64_t seed;
+  const Ctl* ctl;
+  float neg_inv_b;      // dL/dq = -1/B
+  float reg_scale;      // 2 * actor_reg / (B * 5)
+  float* slab;
+  int slab_stride;
+  double* slab_stat;
+};
+
 struct ReduceArgs {
   const float* slab;
   int nwg, slab_stride;
@@ -52,69 +92,7 @@ struct FusedApplyArgs {
   uint32_t* sync_ctr;   // 6 tensor counters of this (agent, net), 32 words apart
   double* sync_part;    // [6][MDP_RA_MAXCH] published sums of squares
   uint32_t* done_ctr;   // workgroups finished (last one advances beta)
-  int dbg;              // timing experiments only (MDP_RA_DBG): 1 no norm handshake, 2 no stats, 8 empty
 };
-// Merged optimizer step (single GPU, fast kernels): the PREVIOUS phase's
-// k_reduce_apply body runs as the `nra` leading workgroups of a gradient
-// kernel launch.  Its chunk workgroups store the net this kernel reads
-// write-through (sc1) -- theta (pub 1: critic step, read by the actor kernel)
-// or the Polyak target (pub 2: actor step, read by the next critic kernel's
-// target actor) -- and add 1 each to *ready; the waves that read that net poll
-// for (ho_seq + 1) * nch first and load it with sc1 loads.  The grid-last
-// workgroup advances Ctl::ho_seq[seq_slot] (and Ctl::upd_ctr when bump_ctr).
-struct MergeArgs {
-  int nra;              // 0: nothing merged
-  int pub;
-  uint32_t* ready;
-  int seq_slot, nch;
-  int wait_agent;       // critic kernel: the target actor whose wave waits (-1: none)
-  int bump_ctr;
-  Ctl* ctl;
-  FusedApplyArgs ra;
-};
-
-struct CriticArgs {
-  Topo topo;
-  int agent, B;
-  const float* theta;
-  const float* target;
-  const float* replay;
-  const int32_t* idx;
-  const float* u_tgt;   // [n][B][5] or null
-  uint64_t seed;
-  const Ctl* ctl;
-  double gamma;
-  float inv_b;
-  float* slab;          // [nwg][slab_stride] partial critic grads (net-relative)
-  int slab_stride;
-  double* slab_stat;    // [nwg][8]
-  double* y_out;        // [B]
-  int group;            // target actors run concurrently per pass (LDS budget)
-  // k_critic_grad_r only: one extra workgroup draws the NEXT round's indices
-  // (pf_count draws into pf_out) while this kernel runs (0: none)
-  Ctl* pf_ctl;
-  int32_t* pf_out;
-  int pf_count;
-  MergeArgs mg;
-};
-
-struct ActorArgs {
-  Topo topo;
-  int agent, B;
-  const float* theta;
-  const float* replay;
-  const int32_t* idx;
-  const float* u_act;   // [B][5] or null
-  uint64_t seed;
-  const Ctl* ctl;
-  float neg_inv_b;      // dL/dq = -1/B
-  float reg_scale;      // 2 * actor_reg / (B * 5)
-  float* slab;
-  int slab_stride;
-  double* slab_stat;
-  MergeArgs mg;
-};
-
 // sync area: per (agent, net) 8 counters x 128 B, then [6][MAXCH] doubles
 inline int64_t mdp_ra_sync_bytes() {
   return (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128 + (int64_t)MDP_MAX_AGENTS * 2 * 6 * MDP_RA_MAXCH * 8;

@@ -58,6 +58,5 @@ struct Ctl {
   int64_t episodes;     // finished episodes logged
   uint32_t ticket[8];   // last-workgroup tickets
   uint32_t upd_ctr;     // RNG counter for training noise
-  uint32_t fault;       // set by a bounded spin that timed out (k_reduce_apply, hand-offs)
-  uint32_t ho_seq[2 * MDP_MAX_AGENTS];  // merged optimizer steps run per (agent, net)
+  uint32_t fault;       // set by a bounded spin that timed out (k_reduce_apply)
 };

@@ -251,51 +251,6 @@ def test_fused_reduce_apply_matches_two_kernel_path(monkeypatch):
         np.testing.assert_allclose(fused1.stats(i), ref1.stats(i), rtol=1e-4, atol=1e-6)
 
 
-def _ctl_u32(eng, off):
-    ctl = eng.region("ctl", torch.uint8).cpu().numpy()
-    return int(ctl[off:off + 4].view(np.uint32)[0])
-
-
-CTL_UPD_CTR_OFFSET = 2568  # Ctl.upd_ctr
-
-
-@pytest.mark.parametrize("dims,local_q", [([18, 18, 18], None), ([4], None), ([8, 10, 10], [True, False, False])])
-def test_merged_optimizer_steps_bit_identical(monkeypatch, dims, local_q):
-    """Merged rounds (each optimizer step runs as leading workgroups of the next
-    gradient launch and hands the stepped net over write-through) are the same
-    arithmetic as separate k_reduce_apply launches: bit-identical parameters,
-    Adam slots, beta powers, stats and noise counter after 4 rounds (hand-offs
-    across agents; across rounds: test_train_step_graph_equals_step_then_rounds),
-    no spin timed out.  Covers N=1 (the critic waits on its own target actor)
-    and a DDPG agent (its critic runs only its own target actor)."""
-    B, L = 256, 4000
-    c = synthetic_trainer_case(dims, B, L, seed=17)
-
-    def run():
-        eng = Engine(dims, local_q, batch_size=B, capacity=L)
-        eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
-        eng.init_params(3)
-        eng.seed_py_random(5)
-        for _ in range(4):
-            eng.update_round()
-        eng.synchronize()
-        return eng
-
-    merged = run()
-    monkeypatch.setenv("MDP_NO_MERGE", "1")
-    plain = run()
-    assert _ctl_u32(merged, CTL_FAULT_OFFSET) == 0
-    assert _ctl_u32(merged, CTL_UPD_CTR_OFFSET) == _ctl_u32(plain, CTL_UPD_CTR_OFFSET) == 4 * len(dims)
-    for i in range(len(dims)):
-        for net in (0, 1):
-            np.testing.assert_array_equal(merged.get_beta_powers(i, net), plain.get_beta_powers(i, net))
-        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_actor", "v_actor", "m_critic", "v_critic"):
-            a, b = merged.get_params(i, w), plain.get_params(i, w)
-            for k in a:
-                np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k}")
-        np.testing.assert_array_equal(merged.stats(i), plain.stats(i))
-
-
 # --------------------------------------------------------------------- env
 SCENARIOS = [("simple", 1, 0), ("simple_spread", 3, 0), ("simple_adversary", 3, 1),
              ("simple_tag", 4, 3), ("simple_tag", 6, 4)]
