@@ -61,9 +61,10 @@ def bytes_rollout(eng):
 
 
 def roofline_for(kind, eng, ms_avg):
+    tp = getattr(eng, "update_mode", "strict") == "throughput"   # one launch serves every agent
     if kind in ("critic_grad", "actor_grad"):
         f = flops_critic_grad if kind == "critic_grad" else flops_actor_grad
-        fl = sum(f(eng, i) for i in range(eng.n)) / eng.n
+        fl = sum(f(eng, i) for i in range(eng.n)) / (1 if tp else eng.n)
         ach = fl / (ms_avg * 1e-3) / 1e12
         suffix = "_r" if eng.lib.mdp_grad_variant(eng.h, 0) == 1 else ""
         return {"bound": "mfma", "achieved": round(ach, 4), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -80,6 +81,8 @@ def roofline_for(kind, eng, ms_avg):
         pc = cin * H + H + H * H + H + H + 1
         nwg = (eng.batch_size + 15) // 16
         by = 4 * ((pc + pa) / 2) * (nwg + 7) + 4 * pa
+        if tp:   # one launch steps every net (2n), each with its own Polyak
+            by = 4 * eng.n * (pc + pa) * (nwg + 8)
     else:
         return None
     ach = by / (ms_avg * 1e-3) / 1e9
@@ -155,6 +158,8 @@ def main():
     ap.add_argument("--num-adversaries", type=int, default=0, help="agents trained with --adv-policy")
     ap.add_argument("--good-policy", default="maddpg")
     ap.add_argument("--adv-policy", default="maddpg")
+    ap.add_argument("--update-mode", choices=["strict", "throughput"], default="strict",
+                    help="throughput: SURVEY 8e's round-parallel mode (not the reference's update order)")
     args = ap.parse_args()
 
     world, rank, local = init_process_group_from_env()
@@ -167,6 +172,8 @@ def main():
                   num_units=args.num_units, seed=args.seed, train_every=args.train_every, world_size=world,
                   rank=rank)
     eng = r.eng
+    if args.update_mode != "strict":
+        eng.set_update_mode(args.update_mode)
     r.prefill()
     kinds = [k for k in _lib.KERNEL]
 
@@ -270,7 +277,7 @@ def main():
                                       if any(eng.local_q) else ""),
                        "scenario": args.scenario, "num_envs_per_gpu": args.num_envs,
                        "global_batch": args.batch_size * world, "parallelism": f"dp{world}",
-                       "mode": "rollout-only" if args.rollout_only else "strict"},
+                       "mode": "rollout-only" if args.rollout_only else args.update_mode},
             "trainer_updates_per_sec": round(updates / dt, 3),
             "rounds_per_sec": round(rounds / dt, 3),
             "rollout_only_env_steps_per_sec": round(rollout_only, 3),

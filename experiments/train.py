@@ -63,6 +63,9 @@ def parse_args(argv=None):
     parser.add_argument("--num-agents", type=int, default=None, help="scenario agent count override")
     parser.add_argument("--scenario-adversaries", type=int, default=None, help="adversaries in the scenario world")
     parser.add_argument("--train-every", type=int, default=100, help="transitions per update round (maddpg.py:164)")
+    parser.add_argument("--update-mode", choices=["strict", "throughput"], default="strict",
+                        help="strict: the reference's update order; throughput: every agent's gradients from "
+                             "the round-start parameters, then every optimizer step (SURVEY 8e, single GPU)")
     return parser.parse_args(argv)
 
 
@@ -126,6 +129,8 @@ def train(arglist):
                        num_units=arglist.num_units, lr=arglist.lr, gamma=arglist.gamma,
                        max_episode_len=arglist.max_episode_len, seed=arglist.seed,
                        train_every=arglist.train_every, world_size=world, rank=rank)
+    if arglist.update_mode != "strict":
+        runner.eng.set_update_mode(arglist.update_mode)
     n = runner.n
     num_adversaries = min(n, arglist.num_adversaries)
     say = (lambda *a: print(*a, flush=True)) if rank == 0 else (lambda *a: None)

@@ -187,6 +187,21 @@ int mdp_apply_grad(mdp_handle* h, int32_t agent, int32_t net, float scale);
 /* the 6 values update() returns (maddpg.py:196), fp64, synchronises */
 int mdp_get_stats(mdp_handle* h, int32_t agent, double out6[6]);
 
+/* ---- update mode of the round paths (mdp_update_round, mdp_train_step) ----
+ * 0 strict (default): the reference's order -- agents in turn, each critic
+ *   step before its actor step, later agents' TD targets see the earlier
+ *   agents' Polyak-updated target actors (maddpg.py:180-194, train.py:160-161).
+ * 1 throughput (opt-in, NOT the reference's semantics): every
+ *   agent's critic and actor gradients from the round-start parameters, then
+ *   every clip + Adam + Polyak -- 3 launches per round.  Single GPU; needs the
+ *   fast H=64 kernels (mdp_grad_variant == 1) for every agent. */
+int mdp_set_update_mode(mdp_handle* h, int32_t mode);
+/* one throughput-mode round with injected randomness (the parity entry point,
+ * like mdp_update): idx_dev [n][B] (NULL: drawn from the index stream),
+ * u_tgt_dev [n][n][B][5] (agent, target actor j, row), u_act_dev [n][B][5]
+ * (NULL: device Philox noise, counter upd_ctr + agent) */
+int mdp_update_all(mdp_handle* h, const int32_t* idx_dev, const float* u_tgt_dev, const float* u_act_dev);
+
 /* ---- device environments (MPE World.step, train.py:104-128) ---------- */
 int mdp_env_reset(mdp_handle* h);
 /* one vector step: actions from the actors (or act_in_dev [E][n][5]), physics,

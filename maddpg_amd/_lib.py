@@ -117,6 +117,8 @@ SIGNATURES = {
     "mdp_env_set_state": (ctypes.c_int, [_P, _F32P, _F32P, _I32P, _I32P]),
     "mdp_env_obs": (ctypes.c_int, [_P, _P]),
     "mdp_env_step_bench": (ctypes.c_int, [_P, _P]),
+    "mdp_set_update_mode": (ctypes.c_int, [_P, _I32]),
+    "mdp_update_all": (ctypes.c_int, [_P, _P, _P, _P]),
     "mdp_episode_count": (_I64, [_P]),
     "mdp_episode_log": (ctypes.c_int, [_P, _I64, _I64, _F32P]),
     "mdp_prof_enable": (ctypes.c_int, [_P, _I32, _I32]),

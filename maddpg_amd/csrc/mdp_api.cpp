@@ -194,8 +194,10 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   sz[MDP_R_ENV] = (int64_t)E * (4 * 4 * L.n_ent + 4 + 4 + 4 * n) + 64;
   sz[MDP_R_EPLOG] = 4 * (int64_t)L.eplog_rows * (1 + n);
   sz[MDP_R_BETA] = 4 * 8 * (int64_t)n;  // per optimizer: next powers (TF vars), powers of this step
-  sz[MDP_R_SLAB] = 4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg + 8 * (int64_t)c->batch_size + 256 +
-                   256 + mdp_ra_sync_bytes();
+  // per-agent blocks of partial gradients / stats / TD targets (throughput mode
+  // computes every agent's gradients in one launch; strict mode uses block 0)
+  sz[MDP_R_SLAB] = (int64_t)n * (4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg +
+                                  8 * (int64_t)c->batch_size) + 256 + 256 + mdp_ra_sync_bytes();
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
   for (int r = 0; r < MDP_R_COUNT; ++r) {
@@ -284,6 +286,10 @@ struct mdp_handle {
   ncclComm_t comm = nullptr;
   int dp_world = 1;
   bool dp_graphs = false;  // capture collectives in the step graph (MDP_DP_GRAPHS=1)
+  // update mode of the round paths: 0 strict (maddpg.py order), 1 throughput
+  int update_mode = 0;
+  FusedApplyArgs* tp_list = nullptr;  // device copy of the 2n optimizer steps (throughput mode)
+  RaBatch tp_batch;
 };
 
 namespace {
@@ -388,6 +394,8 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
 
 int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr) {
   CriticArgs a;
+  a.multi = 0;
+  a.slab_agent_stride = 0;
   a.pf_ctl = h->ctl;
   a.pf_out = nullptr;
   a.pf_count = 0;
@@ -428,6 +436,8 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
 
 int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act) {
   ActorArgs a;
+  a.multi = 0;
+  a.slab_agent_stride = 0;
   a.topo = h->L.topo;
   a.agent = agent;
   a.B = h->cfg.batch_size;
@@ -512,7 +522,7 @@ bool reduce_apply_ok(const mdp_handle* h, int agent, int net) {
   return true;
 }
 
-int do_reduce_apply(mdp_handle* h, int agent, int net) {
+FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net) {
   FusedApplyArgs f;
   f.ap = apply_args(h, agent, net, 1.0f);
   f.ap.slab = net ? h->slab_c : h->slab_a;
@@ -523,6 +533,11 @@ int do_reduce_apply(mdp_handle* h, int agent, int net) {
   f.sync_ctr = h->ra_ctr + (int64_t)g * 8 * 32;
   f.done_ctr = f.sync_ctr + 6 * 32;
   f.sync_part = h->ra_part + (int64_t)g * 6 * MDP_RA_MAXCH;
+  return f;
+}
+
+int do_reduce_apply(mdp_handle* h, int agent, int net) {
+  const FusedApplyArgs f = fused_args_for(h, agent, net);
   ProfScope p(h, MDP_K_REDUCE_APPLY);
   HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
   return 0;
@@ -624,6 +639,112 @@ int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, 
   return 0;
 }
 
+// ---- throughput mode: every agent's critic and actor gradients
+// from the round-start parameters (one launch each), then every optimizer
+// step (clip + Adam + Polyak) in one launch.  NOT the reference's order
+// (maddpg.py:188-194, train.py:160-161): labelled, opt-in.
+bool tp_ok(const mdp_handle* h) {
+  if (h->general_grads || !h->fused_apply) return false;
+  for (int i = 0; i < h->cfg.n_agents; ++i)
+    if (!grads_r_ok(h->L.topo, i) || !reduce_apply_ok(h, i, 0) || !reduce_apply_ok(h, i, 1)) return false;
+  return 2 * h->cfg.n_agents <= MDP_RA_BATCH_MAX;
+}
+
+// the optimizer step of (agent, net) in throughput mode: its own block of
+// partials / stats, Polyak of its own net (both nets stepped in this launch),
+// agent 0's actor step advances the noise counter by n (every agent used
+// upd_ctr + agent)
+FusedApplyArgs tp_args(mdp_handle* h, int agent, int net) {
+  const int64_t nwg = h->L.nwg;
+  FusedApplyArgs f = fused_args_for(h, agent, net);
+  f.ap.slab = net ? h->slab_c + agent * nwg * h->L.slab_c : h->slab_a + agent * nwg * h->L.slab_a;
+  f.ap.slab_stat = (net ? h->stat_c : h->stat_a) + agent * nwg * 8;
+  f.ap.y = h->y + (int64_t)agent * h->cfg.batch_size;
+  f.ap.polyak = 1;
+  for (int t = 0; t < 7; ++t) f.ap.oblk[t] = 0;
+  f.ap.bump_ctr = (net == 0 && agent == 0) ? h->cfg.n_agents : 0;
+  return f;
+}
+
+int tp_setup(mdp_handle* h) {
+  if (h->tp_list) return 0;
+  const int n = h->cfg.n_agents;
+  std::vector<FusedApplyArgs> list;
+  RaBatch& rb = h->tp_batch;
+  rb.count = 2 * n;
+  rb.wg_start[0] = 0;
+  for (int i = 0; i < n; ++i)
+    for (int net = 1; net >= 0; --net) {
+      list.push_back(tp_args(h, i, net));
+      const int q = (int)list.size() - 1;
+      rb.wg_start[q + 1] = rb.wg_start[q] + mdp_ra_grid(list.back());
+    }
+  HIPCHK(h, hipMalloc((void**)&h->tp_list, sizeof(FusedApplyArgs) * list.size()));
+  HIPCHK(h, hipMemcpy(h->tp_list, list.data(), sizeof(FusedApplyArgs) * list.size(), hipMemcpyHostToDevice));
+  rb.list = h->tp_list;
+  return 0;
+}
+
+// every agent's gradients + every optimizer step; idx [n][B]; optional injected
+// uniforms u_tgt [n][n][B][5] (agent, target actor j, row) and u_act [n][B][5]
+int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
+  const int n = h->cfg.n_agents;
+  const int64_t nwg = h->L.nwg;
+  int lds_c = 0;
+  for (int i = 0; i < n; ++i) lds_c = std::max(lds_c, lds_critic_r_bytes(h->L.topo, i));
+  {
+    CriticArgs a;
+    a.pf_ctl = h->ctl;
+    a.pf_out = pf_out;
+    a.pf_count = pf_out ? n * h->cfg.batch_size : 0;
+    a.topo = h->L.topo;
+    a.agent = 0;
+    a.B = h->cfg.batch_size;
+    a.theta = h->theta;
+    a.target = h->target;
+    a.replay = h->replay;
+    a.idx = idx;
+    a.u_tgt = u_tgt;
+    a.seed = h->cfg.seed;
+    a.ctl = h->ctl;
+    a.gamma = h->cfg.gamma;
+    a.inv_b = 1.0f / (float)a.B;
+    a.slab = h->slab_c;
+    a.slab_stride = h->L.slab_c;
+    a.slab_stat = h->stat_c;
+    a.y_out = h->y;
+    a.group = 0;
+    a.multi = n;
+    a.slab_agent_stride = nwg * h->L.slab_c;
+    ProfScope p(h, MDP_K_CRITIC_GRAD);
+    HIPCHK(h, mdp_launch_critic_grad_r(a, lds_c, h->stream));
+  }
+  {
+    ActorArgs a;
+    a.topo = h->L.topo;
+    a.agent = 0;
+    a.B = h->cfg.batch_size;
+    a.theta = h->theta;
+    a.replay = h->replay;
+    a.idx = idx;
+    a.u_act = u_act;
+    a.seed = h->cfg.seed;
+    a.ctl = h->ctl;
+    a.neg_inv_b = -1.0f / (float)a.B;
+    a.reg_scale = (float)(2.0 * (double)h->cfg.actor_reg / ((double)a.B * MDP_ACT_DIM));
+    a.slab = h->slab_a;
+    a.slab_stride = h->L.slab_a;
+    a.slab_stat = h->stat_a;
+    a.multi = n;
+    a.slab_agent_stride = nwg * h->L.slab_a;
+    ProfScope p(h, MDP_K_ACTOR_GRAD);
+    HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
+  }
+  ProfScope p(h, MDP_K_REDUCE_APPLY);
+  HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_batch, h->stream));
+  return 0;
+}
+
 int set_ring(mdp_handle* h, int64_t len, int64_t next) {
   h->len = len;
   h->next = next;
@@ -705,18 +826,18 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
   }
   {
     char* p = (char*)R(MDP_R_SLAB);
-    const int64_t nwg = h->L.nwg;
+    const int64_t nwg = h->L.nwg, na = cfg->n_agents;
     h->slab_c = (float*)p;
-    p += 4 * nwg * h->L.slab_c;
+    p += 4 * na * nwg * h->L.slab_c;
     h->slab_a = (float*)p;
-    p += 4 * nwg * h->L.slab_a;
+    p += 4 * na * nwg * h->L.slab_a;
     p = (char*)(((uintptr_t)p + 7) & ~uintptr_t(7));
     h->stat_c = (double*)p;
-    p += 8 * 8 * nwg;
+    p += 8 * 8 * na * nwg;
     h->stat_a = (double*)p;
-    p += 8 * 8 * nwg;
+    p += 8 * 8 * na * nwg;
     h->y = (double*)p;
-    p += 8 * (int64_t)cfg->batch_size + 256;
+    p += 8 * na * (int64_t)cfg->batch_size + 256;
     p = (char*)(((uintptr_t)p + 255) & ~uintptr_t(255));
     h->ra_ctr = (uint32_t*)p;
     h->ra_part = (double*)(p + (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128);
@@ -740,6 +861,7 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
 int mdp_destroy(mdp_handle* h) {
   if (!h) return 0;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->tp_list) (void)hipFree(h->tp_list);
   for (int k = 0; k < MDP_K_COUNT; ++k)
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->round_exec) (void)hipGraphExecDestroy(h->round_exec);
@@ -989,6 +1111,7 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
 
 static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nullptr) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
+  if (h->update_mode == 1) return do_round_tp(h, idx, nullptr, nullptr, pf_out);
   int rc = 0;
   for (int i = 0; i < n && !rc; ++i) rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, i == 0 ? pf_out : nullptr);
   return rc;
@@ -1055,6 +1178,7 @@ int mdp_dp_unique_id(uint8_t* out128) {
 }
 
 int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank) {
+  if (h && h->update_mode != 0) return fail(h, "data parallelism runs the strict update mode");
   if (!h || !id128) return -1;
   if (!rccl().ok) return fail(h, "librccl.so.1 could not be loaded");
   if (world < 1 || rank < 0 || rank >= world) return fail(h, "mdp_dp_init: bad world/rank");
@@ -1088,6 +1212,51 @@ int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank
 int mdp_set_graphs(mdp_handle* h, int32_t on) {
   h->graphs = on != 0;
   return 0;
+}
+
+static void drop_graphs(mdp_handle* h) {
+  for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
+  h->step_exec.clear();
+  h->eager_steps = 0;
+  if (h->round_exec) {
+    (void)hipGraphExecDestroy(h->round_exec);
+    h->round_exec = nullptr;
+  }
+  if (h->round_graph) {
+    (void)hipGraphDestroy(h->round_graph);
+    h->round_graph = nullptr;
+  }
+  h->eager_rounds = 0;
+}
+
+int mdp_set_update_mode(mdp_handle* h, int32_t mode) {
+  if (!h) return -1;
+  if (mode != 0 && mode != 1) return fail(h, "update mode must be 0 (strict) or 1 (throughput)");
+  if (mode == 1) {
+    if (h->comm) return fail(h, "throughput mode is single-GPU in this build");
+    if (!tp_ok(h)) return fail(h, "throughput mode needs the fast H=64 kernels for every agent");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (tp_setup(h)) return -1;
+  }
+  if (mode != h->update_mode) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    drop_graphs(h);
+    h->update_mode = mode;
+  }
+  return 0;
+}
+
+int mdp_update_all(mdp_handle* h, const int32_t* idx_dev, const float* u_tgt_dev, const float* u_act_dev) {
+  if (!h) return -1;
+  if (h->update_mode != 1) return fail(h, "mdp_update_all: set throughput mode first");
+  if (h->len <= 0) return fail(h, "update on an empty replay buffer");
+  const int32_t* idx = idx_dev;
+  if (!idx) {
+    const int rc = launch_make_index(h, h->cfg.n_agents * h->cfg.batch_size, h->index);
+    if (rc) return rc;
+    idx = h->index;
+  }
+  return do_round_tp(h, idx, u_tgt_dev, u_act_dev, nullptr);
 }
 
 int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev) {

@@ -33,10 +33,10 @@ __device__ __forceinline__ double ld_agent(const double* p) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
+// b: this workgroup's index among the nb workgroups of this net's step
+__device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const int b, const uint32_t nb) {
   const ApplyArgs& a = f.ap;
   __shared__ f32x4 red[16][64];
-  const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   if (b < f.rblk[6]) {
     int t = 0;
@@ -183,7 +183,6 @@ __global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
   // workgroup read beta before its add, so nobody reads the new values here)
   __syncthreads();
   if (tid == 0) {
-    const uint32_t nb = gridDim.x;
     const uint32_t prev = __hip_atomic_fetch_add(f.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev % nb == nb - 1) {
       const float p1 = a.beta[0], p2 = a.beta[1];
@@ -191,14 +190,35 @@ __global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
       a.beta[3] = p2;
       a.beta[0] = p1 * a.b1;
       a.beta[1] = p2 * a.b2;
-      if (a.bump_ctr) a.ctl->upd_ctr += 1u;
+      if (a.bump_ctr) a.ctl->upd_ctr += (uint32_t)a.bump_ctr;
     }
   }
 }
 
-hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
+__global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
+  reduce_apply_body(f, blockIdx.x, gridDim.x);
+}
+
+// throughput mode: the steps of several nets in one launch (each net's chunk
+// workgroups handshake only among themselves; the nets are independent)
+__global__ __launch_bounds__(1024) void k_reduce_apply_batch(RaBatch rb) {
+  int q = 0;
+  while (q + 1 < rb.count && (int)blockIdx.x >= rb.wg_start[q + 1]) ++q;
+  const int b = blockIdx.x - rb.wg_start[q];
+  reduce_apply_body(rb.list[q], b, (uint32_t)(rb.wg_start[q + 1] - rb.wg_start[q]));
+}
+
+int mdp_ra_grid(const FusedApplyArgs& f) {
   const ApplyArgs& a = f.ap;
-  const int grid = f.rblk[6] + (a.polyak ? a.oblk[6] : 0) + (a.stats_mode ? 1 : 0);
-  hipLaunchKernelGGL(k_reduce_apply, dim3(grid), dim3(1024), 0, s, f);
+  return f.rblk[6] + (a.polyak ? a.oblk[6] : 0) + (a.stats_mode ? 1 : 0);
+}
+
+hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_apply, dim3(mdp_ra_grid(f)), dim3(1024), 0, s, f);
+  return hipGetLastError();
+}
+
+hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_apply_batch, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
   return hipGetLastError();
 }

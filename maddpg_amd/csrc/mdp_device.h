@@ -263,9 +263,13 @@ __device__ __forceinline__ void tile_head(const float* X, int ldx, int K, const 
 // softmax(logits - log(-log(u))) on one row of 5 (distributions.py:264-266)
 // Gumbel noise g = log(-log(u)) (distributions.py:235) -- independent of the
 // logits, so the fast kernels compute it while their weights are in flight
+// The noise and the softmax use the hardware transcendentals (v_log_f32 /
+// v_exp_f32 / v_rcp_f32, a few ulp): the precise libm forms cost ~1 us of VALU
+// in the gradient kernels' prologue, on the critical path.  Parity with the
+// oracle is within the tests' fp32 tolerances either way.
 __device__ __forceinline__ void gumbel_noise5(const float* u, float* gn) {
 #pragma unroll
-  for (int k = 0; k < MDP_ACT_DIM; ++k) gn[k] = logf(-logf(u[k]));
+  for (int k = 0; k < MDP_ACT_DIM; ++k) gn[k] = __logf(-__logf(u[k]));
 }
 // softmax(logits - g): the same operations in the same order as gumbel_softmax5
 __device__ __forceinline__ void gumbel_softmax5_pre(const float* logits, const float* gn, float* a) {
@@ -279,11 +283,12 @@ __device__ __forceinline__ void gumbel_softmax5_pre(const float* logits, const f
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < MDP_ACT_DIM; ++k) {
-    z[k] = expf(z[k] - m);
+    z[k] = __expf(z[k] - m);
     s += z[k];
   }
+  const float inv = __builtin_amdgcn_rcpf(s);
 #pragma unroll
-  for (int k = 0; k < MDP_ACT_DIM; ++k) a[k] = z[k] / s;
+  for (int k = 0; k < MDP_ACT_DIM; ++k) a[k] = z[k] * inv;
 }
 __device__ __forceinline__ void gumbel_softmax5(const float* logits, const float* u, float* a) {
   float gn[MDP_ACT_DIM];

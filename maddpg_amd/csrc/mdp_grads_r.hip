@@ -68,8 +68,16 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   }
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;  // gather waves done (LDS hand-off, replaces a barrier)
+  int agent = a.agent, bx = blockIdx.x;
+  if (a.multi > 1) {  // throughput mode: every agent's critic step in this launch
+    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    agent = bx / nwg;
+    bx -= agent * nwg;
+  }
+  const int32_t* idx = a.multi > 1 ? a.idx + (int64_t)agent * a.B : a.idx;
+  const float* u_tgt = (a.multi > 1 && a.u_tgt) ? a.u_tgt + (int64_t)agent * a.topo.n * a.B * MDP_ACT_DIM : a.u_tgt;
   const Topo& T = a.topo;
-  const ADesc& ag = T.ag[a.agent];
+  const ADesc& ag = T.ag[agent];
   const NDesc& nd = ag.critic;
   const bool lq = ag.local_q != 0;
   const int na = lq ? 1 : T.n;
@@ -98,12 +106,15 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const int r0 = blockIdx.x * MDP_R;
+  const int r0 = bx * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
-  const uint32_t ctr = a.ctl->upd_ctr;
+  const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)agent : 0u);
   const float* Pc = a.theta;
   const float* Pt = a.target;
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
+  const int64_t ao = a.multi > 1 ? (int64_t)agent : 0;  // per-agent output blocks (throughput mode)
+  float* slab = a.slab + ao * a.slab_agent_stride + (int64_t)bx * a.slab_stride - nd.off;
+  double* slab_stat = a.slab_stat + ao * (int64_t)((a.B + MDP_R - 1) / MDP_R) * 8;
+  double* y_out = a.y_out + ao * a.B;
   MDP_STAMP(0);
   if (threadIdx.x == 0) rows_ready = 0;
   __syncthreads();  // B0 (nothing in flight yet)
@@ -112,7 +123,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     f32x4 wt[4];  // W2^T tile of the critic for dh1 (loaded once this wave's forward weights are dead)
     if (wave < na) {
       // ---------------- target actor j on obs'_j, Gumbel-softmax target action (maddpg.py:183)
-      const int j = lq ? a.agent : wave;
+      const int j = lq ? agent : wave;
       const ADesc& aj = T.ag[j];
       const NDesc& an = aj.actor;
 #ifdef MDP_STAMPS
@@ -135,11 +146,11 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       float gn[MDP_ACT_DIM];
       {
         float u[MDP_ACT_DIM];
-        if (a.u_tgt) {
+        if (u_tgt) {
           for (int k = 0; k < MDP_ACT_DIM; ++k)
-            u[k] = lane < nvalid ? a.u_tgt[((int64_t)j * a.B + r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
+            u[k] = lane < nvalid ? u_tgt[((int64_t)j * a.B + r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
         } else {
-          uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
+          uniforms5(a.seed, (uint32_t)((agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
         }
         gumbel_noise5(u, gn);
       }
@@ -240,7 +251,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     const int tt = wave - 4, col = 16 * tt + r;
     // the replay gather is issued first, by these waves only (their own weights are few
     // and needed late); waves 0..3 start on their weight loads at once
-    gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 256, 256);
+    gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 256, 256);
     lds_signal(&rows_ready);
 #ifdef MDP_STAMPS
     if (tt == 0) {
@@ -291,7 +302,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         s_y = y64;
         s_r = rew;
         s_q = qnv;
-        a.y_out[r0 + lane] = y64;
+        y_out[r0 + lane] = y64;
       }
       if (lane < MDP_R) dq[lane] = g;
       s_l = sum16(s_l);
@@ -299,7 +310,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       s_r = sum16(s_r);
       s_q = sum16(s_q);
       if (lane == 0) {
-        double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+        double* st = slab_stat + (int64_t)bx * 8;
         st[0] = s_l;
         st[1] = s_y;
         st[2] = s_r;
@@ -337,8 +348,16 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;
+  int agent = a.agent, bx = blockIdx.x;
+  if (a.multi > 1) {  // throughput mode: every agent's actor step in this launch
+    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    agent = bx / nwg;
+    bx -= agent * nwg;
+  }
+  const int32_t* idx = a.multi > 1 ? a.idx + (int64_t)agent * a.B : a.idx;
+  const float* u_act = (a.multi > 1 && a.u_act) ? a.u_act + (int64_t)agent * a.B * MDP_ACT_DIM : a.u_act;
   const Topo& T = a.topo;
-  const ADesc& ag = T.ag[a.agent];
+  const ADesc& ag = T.ag[agent];
   const NDesc& na = ag.actor;
   const NDesc& nc = ag.critic;
   const bool lq = ag.local_q != 0;
@@ -363,11 +382,13 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
-  const int r0 = blockIdx.x * MDP_R;
+  const int r0 = bx * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
-  const uint32_t ctr = a.ctl->upd_ctr;
+  const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)agent : 0u);
   const float* P = a.theta;
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
+  const int64_t ao = a.multi > 1 ? (int64_t)agent : 0;
+  float* slab = a.slab + ao * a.slab_agent_stride + (int64_t)bx * a.slab_stride - na.off;
+  double* slab_stat = a.slab_stat + ao * (int64_t)((a.B + MDP_R - 1) / MDP_R) * 8;
   MDP_STAMP(16);
   if (threadIdx.x == 0) rows_ready = 0;
   __syncthreads();  // B0
@@ -385,11 +406,11 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       float gn[MDP_ACT_DIM];  // Gumbel noise of the policy sample, while the weights are in flight
       {
         float u[MDP_ACT_DIM];
-        if (a.u_act) {
+        if (u_act) {
           for (int k = 0; k < MDP_ACT_DIM; ++k)
-            u[k] = lane < nvalid ? a.u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
+            u[k] = lane < nvalid ? u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
         } else {
-          uniforms5(a.seed, (uint32_t)((a.agent << 8) | 0x80), ctr, (uint32_t)(r0 + (lane & 15)), u);
+          uniforms5(a.seed, (uint32_t)((agent << 8) | 0x80), ctr, (uint32_t)(r0 + (lane & 15)), u);
         }
         gumbel_noise5(u, gn);
       }
@@ -456,7 +477,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       s_q = sum16(s_q);
       s_p = sum16(s_p);
       if (lane == 0) {
-        double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+        double* st = slab_stat + (int64_t)bx * 8;
         st[0] = s_q;
         st[1] = s_p;
       }
@@ -520,7 +541,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       __syncthreads();  // B4
       __syncthreads();  // B5
     } else {
-      gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 128, 384);
+      gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
       lds_signal(&rows_ready);
       __syncthreads();  // B2
       __syncthreads();  // B3
@@ -535,7 +556,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     // ---------------- dgrad tiles: dh1c through the critic, dh1a through the actor
     const int tt = wave - 4;
     // waves 2..7 gather the replay rows (first); waves 0, 1 start on their weights at once
-    gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 128, 384);
+    gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
     lds_signal(&rows_ready);
     f32x4 wc[4], wa[4];
     rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);
@@ -566,7 +587,8 @@ hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr, int 
     (void)hipGetLastError();
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3((a.B + MDP_R - 1) / MDP_R + extra), dim3(512), lds, s, a);
+  const int per = (a.B + MDP_R - 1) / MDP_R;
+  hipLaunchKernelGGL(kern, dim3(per * (a.multi > 1 ? a.multi : 1) + extra), dim3(512), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace

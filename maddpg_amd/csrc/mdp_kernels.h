@@ -27,6 +27,11 @@ struct CriticArgs {
   Ctl* pf_ctl;
   int32_t* pf_out;
   int pf_count;
+  // throughput mode (fast kernels): `multi` agents in one launch, agent =
+  // workgroup / (B/16); idx, u_tgt, slab, slab_stat, y_out are then bases with
+  // per-agent strides and the noise counter is upd_ctr + agent
+  int multi;
+  int64_t slab_agent_stride;
 };
 
 struct ActorArgs {
@@ -43,6 +48,8 @@ struct ActorArgs {
   float* slab;
   int slab_stride;
   double* slab_stat;
+  int multi;                  // throughput mode, as CriticArgs
+  int64_t slab_agent_stride;
 };
 
 struct ReduceArgs {
@@ -80,7 +87,7 @@ struct ApplyArgs {
   double* stats_out;
   uint32_t* ticket;
   Ctl* ctl;
-  int bump_ctr;
+  int bump_ctr;         // the last workgroup advances Ctl::upd_ctr by this much
 };
 
 // k_reduce_apply (mdp_apply_fused.hip): batch reduction + optimizer step in one launch
@@ -209,6 +216,16 @@ hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t 
 hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s);
 hipError_t mdp_launch_reduce(const ReduceArgs& a, hipStream_t s);
 hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s);
+// throughput mode: the optimizer steps of `count` nets in one launch; list[]
+// lives in device memory (written once), wg_start[q] = first workgroup of net q
+#define MDP_RA_BATCH_MAX (2 * MDP_MAX_AGENTS)
+struct RaBatch {
+  const FusedApplyArgs* list;
+  int count;
+  int wg_start[MDP_RA_BATCH_MAX + 1];
+};
+int mdp_ra_grid(const FusedApplyArgs& f);
+hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s);
 hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t s);
 hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
                              hipStream_t s);

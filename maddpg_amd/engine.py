@@ -33,6 +33,7 @@ class Engine:
         self.n = n
         self.obs_dims = [int(o) for o in obs_dims]
         self.local_q = [bool(x) for x in local_q]
+        self.update_mode = "strict"
         self.num_units = int(num_units)
         self.batch_size = int(batch_size)
         self.max_episode_len = int(max_episode_len)
@@ -323,6 +324,26 @@ class Engine:
             args.append(None if t is None else t.to(self.device, dt).contiguous())
         self.sync_in()
         self._c("mdp_update", agent, *[self._ptr(a) for a in args])
+        self._keep = args
+        self.sync_out()
+
+    UPDATE_MODES = {"strict": 0, "throughput": 1}
+
+    def set_update_mode(self, mode):
+        """'strict' (the reference's order, default) or 'throughput' (every
+        agent's gradients from the round-start parameters, then every optimizer
+        step: SURVEY.md 8e, not the reference's semantics).  mdp_set_update_mode."""
+        self._c("mdp_set_update_mode", self.UPDATE_MODES[mode])
+        self.update_mode = mode
+
+    def update_all(self, idx=None, u_tgt=None, u_act=None):
+        """one throughput-mode round; idx [n, B], u_tgt [n, n, B, 5], u_act [n, B, 5]
+        (injected randomness for parity; None: device streams).  mdp_update_all."""
+        args = []
+        for t, dt in ((idx, torch.int32), (u_tgt, torch.float32), (u_act, torch.float32)):
+            args.append(None if t is None else t.to(self.device, dt).contiguous())
+        self.sync_in()
+        self._c("mdp_update_all", *[self._ptr(a) for a in args])
         self._keep = args
         self.sync_out()
 

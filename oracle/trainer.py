@@ -128,3 +128,28 @@ def update_batch(agents, i, batch_n, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
     return [st["q_loss"], p_loss, float(np.mean(tq)), float(np.mean(st["rew"])),
             float(np.mean(st["target_q_next"].astype(np.float64))), float(np.std(tq))], \
         {"grad_critic": gq, "grad_actor": gp}
+
+
+def update_round_throughput(agents, buffers, idx_n, u_tgt_n, u_act_n, gamma=0.95, grad_clip=0.5):
+    """Throughput mode -- NOT the reference's order: every
+    agent's critic gradients (targets from the round-start target actors) and
+    actor gradients (against the round-start critic) first, then every clip +
+    Adam + Polyak.  idx_n[i], u_tgt_n[i] (= agent i's u_tgt), u_act_n[i].
+    Returns the per-agent stats lists."""
+    n = len(agents)
+    grads, stats = [], []
+    for i in range(n):
+        batch_n = [tuple(x[idx_n[i]] for x in buffers[j]) for j in range(n)]
+        gq, st = critic_grads(agents, i, batch_n, u_tgt_n[i], gamma)
+        gp, p_loss = actor_grads(agents, i, batch_n, u_act_n[i])
+        grads.append((gq, gp))
+        tq = st["target_q"]
+        stats.append([st["q_loss"], p_loss, float(np.mean(tq)), float(np.mean(st["rew"])),
+                      float(np.mean(st["target_q_next"].astype(np.float64))), float(np.std(tq))])
+    for i, ag in enumerate(agents):
+        gq, gp = grads[i]
+        apply_grads(ag.opt_critic, ag.critic, gq, grad_clip)
+        apply_grads(ag.opt_actor, ag.actor, gp, grad_clip)
+        nets.polyak(ag.tgt_actor, ag.actor)
+        nets.polyak(ag.tgt_critic, ag.critic)
+    return stats

@@ -191,6 +191,87 @@ def test_update_parity_general_kernels_forced(monkeypatch, local_q):
     _update_parity([18, 18, 18], B=256, L=1200, seed=27, local_q=local_q)
 
 
+@pytest.mark.parametrize("dims,local_q,B", [([18, 18, 18], None, 1024), ([4], None, 512),
+                                            ([8, 10, 10], [True, False, False], 256)])
+def test_throughput_mode_round_parity(dims, local_q, B):
+    """Throughput mode (opt-in): one round = every agent's critic and
+    actor gradients from the round-start parameters, then every clip + Adam +
+    Polyak (mdp_update_all) vs oracle.trainer.update_round_throughput on the
+    same injected indices and uniforms: critic loss within 1e-5 relative,
+    parameters within the fp32 tolerance of the strict-mode parity test."""
+    L = 3000
+    c = synthetic_trainer_case(dims, B, L, seed=61, local_q=local_q)
+    n = len(dims)
+    eng = Engine(dims, c["local_q"], batch_size=B, capacity=L + 7)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    for i, p in enumerate(c["params"]):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            eng.set_params(i, w, p[w])
+    eng.set_update_mode("throughput")
+    agents = [trainer.AgentParams(**copy.deepcopy(p), local_q=c["local_q"][i]) for i, p in enumerate(c["params"])]
+    eng.update_all(idx=torch.from_numpy(c["idx"]), u_tgt=torch.from_numpy(c["u_tgt"]),
+                   u_act=torch.from_numpy(c["u_act"]))
+    want = trainer.update_round_throughput(agents, c["data"], c["idx"], c["u_tgt"], c["u_act"])
+    for i in range(n):
+        got = eng.stats(i)
+        assert abs(got[0] - want[i][0]) <= 1e-5 * abs(want[i][0]) + 1e-7, (i, got[0], want[i][0])
+        np.testing.assert_allclose(got[1:], want[i][1:], rtol=2e-5, atol=2e-6)
+        for w, ref in (("actor", agents[i].actor), ("critic", agents[i].critic),
+                       ("tgt_actor", agents[i].tgt_actor), ("tgt_critic", agents[i].tgt_critic)):
+            dev = eng.get_params(i, w)
+            for k in ref:
+                assert np.max(np.abs(dev[k] - ref[k].reshape(dev[k].shape))) < 2e-4, (i, w, k)
+        for net in (0, 1):
+            bp = eng.get_beta_powers(i, net)
+            opt = agents[i].opt_actor if net == 0 else agents[i].opt_critic
+            assert bp[0] == opt.b1p and bp[1] == opt.b2p
+    assert _ctl_u32(eng, CTL_UPD_CTR_OFFSET) == n           # every agent used upd_ctr + agent
+    assert _ctl_u32(eng, CTL_FAULT_OFFSET) == 0
+    # strict mode again on the same handle: mode switches are clean
+    eng.set_update_mode("strict")
+    eng.update_round()
+    eng.synchronize()
+    assert all(np.all(np.isfinite(eng.stats(i))) for i in range(n))
+
+
+def test_throughput_mode_train_step_graph_equals_eager():
+    """mdp_train_step in throughput mode (rollout + k rounds as one graph) is the
+    same work as env_step + k x update_round in throughput mode."""
+    from maddpg_amd.runner import VecRunner
+
+    def make():
+        r = VecRunner("simple_spread", 64, batch_size=128, capacity=20000, seed=3, train_every=16)
+        r.eng.set_update_mode("throughput")
+        r.prefill()
+        return r
+
+    a, b = make(), make()
+    for _ in range(3):
+        t0 = a.train_step
+        k = a.step()
+        b.rollout()
+        assert b.due_rounds(t0, b.train_step) == k
+        for _ in range(k):
+            b.train_round()
+    a.eng.synchronize()
+    b.eng.synchronize()
+    for i in range(3):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_critic", "v_actor"):
+            pa, pb = a.eng.get_params(i, w), b.eng.get_params(i, w)
+            for key in pa:
+                np.testing.assert_array_equal(pa[key], pb[key])
+        np.testing.assert_array_equal(a.eng.stats(i), b.eng.stats(i))
+
+
+def _ctl_u32(eng, off):
+    ctl = eng.region("ctl", torch.uint8).cpu().numpy()
+    return int(ctl[off:off + 4].view(np.uint32)[0])
+
+
+CTL_UPD_CTR_OFFSET = 2568  # Ctl.upd_ctr (mdp_topo.h)
+CTL_FAULT_OFFSET = 2572    # Ctl.fault
+
+
 def test_update_round_uses_device_index_stream():
     """mdp_update_round draws agent 0's B indices first, then agent 1's ...
     (maddpg.py:167 per agent, train.py:160-161 agent order) from the MT stream."""
@@ -221,8 +302,6 @@ def _rounds_engine(dims, B, L, c, rounds):
     eng.synchronize()
     return eng
 
-
-CTL_FAULT_OFFSET = 2572  # Ctl.fault (mdp_topo.h)
 
 
 def test_fused_reduce_apply_matches_two_kernel_path(monkeypatch):
