@@ -193,8 +193,10 @@ int mdp_get_stats(mdp_handle* h, int32_t agent, double out6[6]);
  *   agents' Polyak-updated target actors (maddpg.py:180-194, train.py:160-161).
  * 1 throughput (opt-in, NOT the reference's semantics): every
  *   agent's critic and actor gradients from the round-start parameters, then
- *   every clip + Adam + Polyak -- 3 launches per round.  Single GPU; needs the
- *   fast H=64 kernels (mdp_grad_variant == 1) for every agent. */
+ *   every clip + Adam + Polyak -- 3 launches per round.  With data parallelism
+ *   (mdp_dp_init BEFORE this call): gradients, a reduce pass, ONE all-reduce
+ *   of the whole gradient region per round, the step pass (x 1/world).  Needs
+ *   the fast H=64 kernels (mdp_grad_variant == 1) for every agent. */
 int mdp_set_update_mode(mdp_handle* h, int32_t mode);
 /* one throughput-mode round with injected randomness (the parity entry point,
  * like mdp_update): idx_dev [n][B] (NULL: drawn from the index stream),

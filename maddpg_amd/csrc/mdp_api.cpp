@@ -289,7 +289,8 @@ struct mdp_handle {
   // update mode of the round paths: 0 strict (maddpg.py order), 1 throughput
   int update_mode = 0;
   FusedApplyArgs* tp_list = nullptr;  // device copy of the 2n optimizer steps (throughput mode)
-  RaBatch tp_batch;
+  RaBatch tp_batch;                   // single GPU: reduce + step
+  RaBatch tp_reduce, tp_step;         // data parallel: reduce pass, all-reduce, step pass (x 1/G)
 };
 
 namespace {
@@ -533,6 +534,7 @@ FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net) {
   f.sync_ctr = h->ra_ctr + (int64_t)g * 8 * 32;
   f.done_ctr = f.sync_ctr + 6 * 32;
   f.sync_part = h->ra_part + (int64_t)g * 6 * MDP_RA_MAXCH;
+  f.phase = 0;
   return f;
 }
 
@@ -594,6 +596,16 @@ int dp_allreduce(mdp_handle* h, int agent, int net) {
   const NDesc& d = net_of(h, agent, net);
   float* g = h->grad + d.off;
   const ncclResult_t r = rccl().all_reduce(g, g, (size_t)d.size, ncclFloat32, ncclSum, h->comm, h->stream);
+  if (r != ncclSuccess) {
+    h->err = std::string("ncclAllReduce: ") + rccl().err(r);
+    return -1;
+  }
+  return 0;
+}
+
+// throughput mode: the whole grad region (every agent's actor + critic) in one call
+int dp_allreduce_all(mdp_handle* h) {
+  const ncclResult_t r = rccl().all_reduce(h->grad, h->grad, (size_t)h->L.PT, ncclFloat32, ncclSum, h->comm, h->stream);
   if (r != ncclSuccess) {
     h->err = std::string("ncclAllReduce: ") + rccl().err(r);
     return -1;
@@ -666,24 +678,37 @@ FusedApplyArgs tp_args(mdp_handle* h, int agent, int net) {
   return f;
 }
 
+// three device lists of the 2n steps: [0, 2n) fused (single GPU), [2n, 4n)
+// reduce-only, [4n, 6n) step from the all-reduced grad[] scaled by 1/G
 int tp_setup(mdp_handle* h) {
-  if (h->tp_list) return 0;
+  if (h->tp_list) {
+    (void)hipFree(h->tp_list);
+    h->tp_list = nullptr;
+  }
   const int n = h->cfg.n_agents;
   std::vector<FusedApplyArgs> list;
-  RaBatch& rb = h->tp_batch;
-  rb.count = 2 * n;
-  rb.wg_start[0] = 0;
-  for (int i = 0; i < n; ++i)
-    for (int net = 1; net >= 0; --net) {
-      list.push_back(tp_args(h, i, net));
-      const int q = (int)list.size() - 1;
-      rb.wg_start[q + 1] = rb.wg_start[q] + mdp_ra_grid(list.back());
-    }
+  RaBatch* rbs[3] = {&h->tp_batch, &h->tp_reduce, &h->tp_step};
+  for (int ph = 0; ph < 3; ++ph) {
+    RaBatch& rb = *rbs[ph];
+    rb.count = 2 * n;
+    rb.wg_start[0] = 0;
+    for (int i = 0; i < n; ++i)
+      for (int net = 1; net >= 0; --net) {
+        FusedApplyArgs f = tp_args(h, i, net);
+        f.phase = ph;
+        if (ph == 2) f.ap.scale = 1.0f / (float)h->dp_world;
+        list.push_back(f);
+        const int q = 2 * i + (1 - net);
+        rb.wg_start[q + 1] = rb.wg_start[q] + mdp_ra_grid(f);
+      }
+  }
   HIPCHK(h, hipMalloc((void**)&h->tp_list, sizeof(FusedApplyArgs) * list.size()));
   HIPCHK(h, hipMemcpy(h->tp_list, list.data(), sizeof(FusedApplyArgs) * list.size(), hipMemcpyHostToDevice));
-  rb.list = h->tp_list;
+  for (int ph = 0; ph < 3; ++ph) rbs[ph]->list = h->tp_list + (int64_t)ph * 2 * n;
   return 0;
 }
+
+int dp_allreduce_all(mdp_handle* h);
 
 // every agent's gradients + every optimizer step; idx [n][B]; optional injected
 // uniforms u_tgt [n][n][B][5] (agent, target actor j, row) and u_act [n][B][5]
@@ -739,6 +764,17 @@ int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const flo
     a.slab_agent_stride = nwg * h->L.slab_a;
     ProfScope p(h, MDP_K_ACTOR_GRAD);
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
+  }
+  if (h->comm) {  // data parallel: ONE all-reduce of every net's gradient per round
+    {
+      ProfScope p(h, MDP_K_REDUCE);
+      HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_reduce, h->stream));
+    }
+    const int rc = dp_allreduce_all(h);
+    if (rc) return rc;
+    ProfScope p(h, MDP_K_APPLY);
+    HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_step, h->stream));
+    return 0;
   }
   ProfScope p(h, MDP_K_REDUCE_APPLY);
   HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_batch, h->stream));
@@ -1178,7 +1214,7 @@ int mdp_dp_unique_id(uint8_t* out128) {
 }
 
 int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank) {
-  if (h && h->update_mode != 0) return fail(h, "data parallelism runs the strict update mode");
+  if (h && h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
   if (!h || !id128) return -1;
   if (!rccl().ok) return fail(h, "librccl.so.1 could not be loaded");
   if (world < 1 || rank < 0 || rank >= world) return fail(h, "mdp_dp_init: bad world/rank");
@@ -1233,7 +1269,6 @@ int mdp_set_update_mode(mdp_handle* h, int32_t mode) {
   if (!h) return -1;
   if (mode != 0 && mode != 1) return fail(h, "update mode must be 0 (strict) or 1 (throughput)");
   if (mode == 1) {
-    if (h->comm) return fail(h, "throughput mode is single-GPU in this build");
     if (!tp_ok(h)) return fail(h, "throughput mode needs the fast H=64 kernels for every agent");
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (tp_setup(h)) return -1;

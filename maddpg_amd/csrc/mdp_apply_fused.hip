@@ -38,6 +38,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
   const ApplyArgs& a = f.ap;
   __shared__ f32x4 red[16][64];
   const int tid = threadIdx.x, lane = tid & 63;
+  if (f.phase == 1 && b >= f.rblk[6]) return;  // reduce-only pass: chunk workgroups only
   if (b < f.rblk[6]) {
     int t = 0;
     while (b >= f.rblk[t + 1]) ++t;
@@ -59,7 +60,9 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       if (a.polyak) tg4 = ld4(a.target + i0);
     }
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    if (act) {
+    if (f.phase == 2) {  // step from the all-reduced gradient in grad[]
+      if (grp == 0 && act) s = ld4(a.grad + i0);
+    } else if (act) {
       const float* base = a.slab + (td.off - a.net.off) + p0;
       f32x4 v[4];
 #pragma unroll
@@ -83,12 +86,13 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
         if (p0 + j < n) ss += (double)gs * (double)gs;
       }
       ss = wave_sum_d(ss);
-      if (act) {
+      if (act && f.phase != 2) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (p0 + j < n) a.grad[i0 + j] = g[j];
       }
       double tot = ss;
+      if (f.phase != 1) {  // phase 1 (data parallel) stops here: the all-reduce follows
       if (nch > 1) {
         double* part = f.sync_part + t * MDP_RA_MAXCH;
         uint32_t* ctr = f.sync_ctr + t * 32;
@@ -133,6 +137,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
           }
         }
       }
+      }  // phase != 1
     }
   } else if (a.polyak && b < f.rblk[6] + a.oblk[6]) {
     const int bb = b - f.rblk[6];
@@ -179,6 +184,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       a.stats_out[1] = -s0 / a.B + (double)a.reg * (s1 / ((double)a.B * MDP_ACT_DIM));
     }
   }
+  if (f.phase == 1) return;  // uniform: the whole grid of a reduce-only pass
   // the last workgroup to finish advances the optimizer step (every net
   // workgroup read beta before its add, so nobody reads the new values here)
   __syncthreads();

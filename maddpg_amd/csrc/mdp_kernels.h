@@ -99,6 +99,7 @@ struct FusedApplyArgs {
   uint32_t* sync_ctr;   // 6 tensor counters of this (agent, net), 32 words apart
   double* sync_part;    // [6][MDP_RA_MAXCH] published sums of squares
   uint32_t* done_ctr;   // workgroups finished (last one advances beta)
+  int phase;            // 0 reduce + step; 1 reduce into grad[] only; 2 step from grad[] (all-reduced)
 };
 // sync area: per (agent, net) 8 counters x 128 B, then [6][MAXCH] doubles
 inline int64_t mdp_ra_sync_bytes() {
