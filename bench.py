@@ -160,6 +160,8 @@ def main():
     ap.add_argument("--adv-policy", default="maddpg")
     ap.add_argument("--update-mode", choices=["strict", "throughput"], default="strict",
                     help="throughput: SURVEY 8e's round-parallel mode (not the reference's update order)")
+    ap.add_argument("--no-throughput-figure", action="store_true",
+                    help="skip the secondary throughput-mode measurement of a strict run")
     args = ap.parse_args()
 
     world, rank, local = init_process_group_from_env()
@@ -236,6 +238,43 @@ def main():
     dominant = max(modelled, key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_pre) if modelled else None
     ms_tot, launches = per_kind[dominant] if dominant else (0.0, 0)
 
+    # secondary figure: the same workload in throughput mode (every
+    # agent's gradients from the round-start parameters, one all-reduce per
+    # round) -- NOT the reference's update order, never `value`
+    tp_fig = None
+    if (args.update_mode == "strict" and not args.rollout_only and not args.no_throughput_figure
+            and (world == 1 or getattr(r, "native_dp", False))):
+        try:
+            eng.set_update_mode("throughput")
+        except Exception as e:  # outside the fast kernels' envelope
+            tp_fig = {"skipped": str(e)[:200]}
+        if tp_fig is None:
+            for _ in range(args.warmup):
+                one_step()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            tp_rounds = 0
+            for _ in range(args.steps):
+                tp_rounds += one_step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            tp_dt = time.perf_counter() - t2
+            if world > 1:
+                t = torch.tensor([tp_dt], dtype=torch.float64, device="cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                tp_dt = float(t.item())
+            eng.set_update_mode("strict")
+            tp_fig = {"env_steps_per_sec": round(args.num_envs * args.steps * world / tp_dt, 3),
+                      "trainer_updates_per_sec": round(tp_rounds * r.n / tp_dt, 3),
+                      "rounds_per_sec": round(tp_rounds / tp_dt, 3),
+                      "ms_per_step": round(tp_dt / args.steps * 1e3, 4),
+                      "note": "throughput update mode (SURVEY 8e): every agent's gradients from the round-start "
+                              "parameters, one optimizer launch (and one all-reduce) per round -- not the "
+                              "reference's update order"}
+
     env_steps = args.num_envs * args.steps * world
     updates = rounds * r.n           # optimiser updates (each on world*B samples)
     value = env_steps / dt
@@ -288,6 +327,7 @@ def main():
                                                        if v[1]},
                             "per_kind_launches": {k: v[1] for k, v in per_kind.items()}},
             "roofline": roof,
+            "throughput_mode": tp_fig,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
