@@ -105,17 +105,16 @@ def event_overhead_ms(stream, pairs=64):
     return ts[len(ts) // 2]
 
 
-def load_traffic(kernel, config_key):
-    """per-launch HBM bytes from a committed rocprofv3 PMC summary (profiles/pmc_*.json)."""
+def load_pmc(kernel, config_key):
+    """the committed rocprofv3 PMC summary of `kernel` (profiles/pmc_traffic.json, written by
+    tools/profile_summary.py): per-launch HBM bytes and the MFMA busy fraction."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return {}
     try:
-        d = json.load(open(path))
-        ent = d.get(config_key, {}).get(kernel)
-        return None if ent is None else ent.get("hbm_bytes_per_launch")
+        return json.load(open(path)).get(config_key, {}).get(kernel) or {}
     except Exception:
-        return None
+        return {}
 
 
 def cpu_baseline(args):
@@ -292,8 +291,13 @@ def main():
     if args.num_agents is not None:
         cfg_key += f"_N{args.num_agents}"
     if roof is not None:
-        tr = load_traffic(roof["kernel"], cfg_key)
-        roof["traffic"] = tr
+        pmc = load_pmc(roof["kernel"], cfg_key)
+        roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+        if pmc.get("mfma_busy_frac") is not None:
+            # SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), profiles/<tag>_mfma.csv
+            roof["mfma_busy_frac_rocprof"] = round(pmc["mfma_busy_frac"], 5)
+        if pmc.get("_source") or pmc:
+            roof["pmc_source"] = "profiles/pmc_traffic.json"
     if rank == 0:
         out = {
             "metric": (f"env-steps/sec (end-to-end at the reference update cadence), {args.scenario} N={r.n}, "

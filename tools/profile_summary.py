@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--bench")
+    ap.add_argument("--mfma", help="rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE pass")
+    ap.add_argument("--clock-ghz", type=float, default=2.3, help="shader clock for the MFMA busy fraction")
     ap.add_argument("--config-key", default=None)
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
@@ -77,7 +79,24 @@ def main():
         allj = json.load(open(path)) if os.path.exists(path) else {}
         allj[key] = dict(out, _source=f"{a.tag}_pmc.csv")
         json.dump(allj, open(path, "w"), indent=1, sort_keys=True)
-    print(json.dumps({"tag": a.tag, "config_key": key, "avg_ns": avg_ns, "pmc": out}, indent=1))
+    mf = {}
+    if a.mfma:
+        busy, gui = counters(a.mfma, "SQ_VALU_MFMA_BUSY_CYCLES"), counters(a.mfma, "GRBM_GUI_ACTIVE")
+        with open(os.path.join(prof, f"{a.tag}_mfma.csv"), "w") as fp:
+            # busy fraction of the chip's 1024 SIMDs over the kernel's average duration
+            fp.write("kernel,avg_ns,SQ_VALU_MFMA_BUSY_CYCLES,GRBM_GUI_ACTIVE,mfma_busy_frac_of_1024_simds\n")
+            for k in sorted(busy):
+                ns = avg_ns.get(k)
+                frac = busy[k] / (ns * 1e-9 * a.clock_ghz * 1e9 * 1024) if ns else None
+                mf[k] = {"mfma_busy_cycles": busy[k], "grbm_gui_active": gui.get(k), "mfma_busy_frac": frac}
+                fp.write(f"{k},{ns or ''},{busy[k]:.0f},{gui.get(k, '')},{'' if frac is None else f'{frac:.5f}'}\n")
+        if key:
+            path = os.path.join(prof, "pmc_traffic.json")
+            allj = json.load(open(path)) if os.path.exists(path) else {}
+            for k, v in mf.items():
+                allj.setdefault(key, {}).setdefault(k, {}).update(v)
+            json.dump(allj, open(path, "w"), indent=1, sort_keys=True)
+    print(json.dumps({"tag": a.tag, "config_key": key, "avg_ns": avg_ns, "pmc": out, "mfma": mf}, indent=1))
 
 
 if __name__ == "__main__":
