@@ -25,7 +25,10 @@
 //   all            dW1, db1
 // k_actor_grad_r (maddpg.py:37-58):
 //   wave 0  actor forward, Gumbel a_i                              | B2
-//   wave 1  critic L1 on the replay part (a_i rows masked) | B2 | + a_i part, L2, q, d2 | B3
+//   waves 1..3  critic L1 on the replay part (a_i rows masked), one third of
+//           the contraction each (waves 2, 3 after their share of the gather) | B2
+//   wave 1  sum of the thirds + a_i part -> h1c                    | B2b
+//   waves 0..3  one 16-column tile each of critic L2, d2c, q partials | B3
 //   waves 4..7  dh1c tiles                                         | B4
 //   wave 0  da = dh1c W1c[a_i]^T, softmax backward + reg -> dlogits, d2a, dW3a, db3a | B5
 //   waves 0..3 dW2a, db2a  ||  waves 4..7 dh1a tiles               | B6
@@ -55,6 +58,28 @@ __device__ __forceinline__ void dgrad_tile(const float* dY, const f32x4 (&w)[4],
   for (int i = 0; i < 4; ++i) {
     const int row = kq * 4 + i;
     dX[row * LD + col] = Hin[row * LH + col] > 0.f ? acc[i] : 0.f;
+  }
+}
+// critic L2 column tile tt (columns 16 tt .. 16 tt + 15) for the actor step:
+// h2 = relu(h1 W2 + b2); d2c = dq W3 masked by h2 > 0 with dq = -1/B (rows past
+// the batch zero); q partial = sum over the tile's columns of h2 W3
+__device__ __forceinline__ void critic_l2_tile(const float* h1, const float (&w2t)[16], float b2t, float w3t, int tt,
+                                               int nvalid, float dq, float* d2, float* qpart) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  rt_acc<16>(acc, h1, LH, RH, w2t);
+  const int col = 16 * tt + r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = kq * 4 + i;
+    const float h = fmaxf(acc[i] + b2t, 0.f);
+    d2[row * LD + col] = (row < nvalid && h > 0.f) ? dq * w3t : 0.f;
+    float s = h * w3t;  // sum over the 16 columns (lanes r of this kq group), fixed order
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    s += __shfl_xor(s, 8, 64);
+    if (r == 0) qpart[tt * MDP_R + row] = s;
   }
 }
 }  // namespace
@@ -374,11 +399,12 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   float* h1a = cv.take(MDP_R * LH);
   float* h2a = cv.take(MDP_R * LH);
   float* h1c = cv.take(MDP_R * LH);
-  float* h2c = cv.take(MDP_R * LH);
   float* d2c = cv.take(MDP_R * LD);
   float* d1c = cv.take(MDP_R * LD);
   float* d2a = cv.take(MDP_R * LD);
   float* d1a = cv.take(MDP_R * LD);
+  float* l1part = cv.take(2 * 64 * 16);  // critic L1 partial accumulators of waves 2, 3
+  float* qpart = cv.take(4 * MDP_R);     // critic head partials of the four L2 column tiles
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
@@ -386,6 +412,8 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   const int nvalid = min(MDP_R, a.B - r0);
   const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)agent : 0u);
   const float* P = a.theta;
+  // critic L1 replay-part contraction split over waves 1..3 (KC rows each)
+  constexpr int KC = 28, KSC = KC / 4;
   const int64_t ao = a.multi > 1 ? (int64_t)agent : 0;
   float* slab = a.slab + ao * a.slab_agent_stride + (int64_t)bx * a.slab_stride - na.off;
   double* slab_stat = a.slab_stat + ao * (int64_t)((a.B + MDP_R - 1) / MDP_R) * 8;
@@ -443,9 +471,16 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
 #pragma unroll
       for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
+      float w2t[16];  // critic L2 column tile 0
+      rt_load<16>(w2t, P + nc.t[2].off, RH, r, RH);
+      const float b2t = P[nc.t[3].off + r], w3t = P[nc.t[4].off + r];
       MDP_STAMP(18);
-      __syncthreads();  // B2: a_i ready
+      __syncthreads();  // B2: a_i and the L1 thirds ready
+      __syncthreads();  // B2b: h1c ready
+      critic_l2_tile(h1c, w2t, b2t, w3t, 0, nvalid, a.neg_inv_b, d2c, qpart);
       __syncthreads();  // B3: critic forward, d2c ready
+      if (lane < MDP_R) qv[lane] = ((qpart[lane] + qpart[MDP_R + lane]) + qpart[2 * MDP_R + lane]) +
+                                   qpart[3 * MDP_R + lane] + P[nc.t[5].off];
       __syncthreads();  // B4: dh1c ready
       MDP_STAMP(23);
       // da[r][k] = sum_h dh1c[r][h] W1c[a_in_off + k][h]
@@ -506,44 +541,46 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       }
       MDP_STAMP(24);
       __syncthreads();  // B5: d2a ready
-    } else if (wave == 1) {
+    } else {
       // ---------------- critic (post-step weights) forward with a_i = the sample (maddpg.py:48-52)
-      f32x4 w1[20], w1b[2], w2[16];
-      float w3[16];
-      rf_load<20>(w1, P + nc.t[0].off, ka_c, ag.a_in_off, ag.a_in_off + MDP_ACT_DIM);
-      rf_load<2>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM, 0, 0);
-      rf_load<16>(w2, P + nc.t[2].off, RH, 0, 0);
-      rq_load(w3, P + nc.t[4].off);
-      const f32x4 b1 = ld4(P + nc.t[1].off + 4 * r), b2 = ld4(P + nc.t[3].off + 4 * r);
-      const float b3 = P[nc.t[5].off];
-      const float w3c = P[nc.t[4].off + lane];
+      // waves 2, 3 gather their share of the replay rows first
+      if (wave > 1) gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
+      if (wave > 1) lds_signal(&rows_ready);
+      const int k0 = KC * (wave - 1);  // this wave's third of the replay-part contraction
+      f32x4 w1[KSC];
+      rf_load<KSC>(w1, P + nc.t[0].off + k0 * RH, max(min(ka_c - k0, KC), 0), ag.a_in_off - k0,
+                   ag.a_in_off + MDP_ACT_DIM - k0);
+      f32x4 w1b[2], b1;
+      if (wave == 1) {
+        rf_load<2>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM, 0, 0);
+        b1 = ld4(P + nc.t[1].off + 4 * r);
+      }
+      float w2t[16];  // critic L2 column tile `wave`
+      rt_load<16>(w2t, P + nc.t[2].off, RH, 16 * wave + r, RH);
+      const float b2t = P[nc.t[3].off + 16 * wave + r], w3t = P[nc.t[4].off + 16 * wave + r];
       lds_wait(&rows_ready, 6);
       f32x4 acc[4];
       rf_zero(acc);
-      rf_acc<20>(acc, rowbuf + xo_c, ldr, ka_c, w1);
-      __syncthreads();  // B2
-      MDP_STAMPW(19);
-      rf_acc<2>(acc, av, 8, MDP_ACT_DIM, w1b);
-      rf_store<true>(acc, b1, h1c, LH);
-      wave_sync();
-      rf_zero(acc);
-      rf_acc<16>(acc, h1c, LH, RH, w2);
-      rf_store<true>(acc, b2, h2c, LH);
-      wave_sync();
-      const float q = rq_head(h2c, LH, w3) + b3;
-      if ((lane & 3) == 0) qv[lane >> 2] = q;
-      // dL/dq = -1/B ; d2c = dq W3c masked by h2c > 0 (rows past the batch zero)
+      if (k0 < ka_c) rf_acc<KSC>(acc, rowbuf + xo_c + k0, ldr, min(ka_c - k0, KC), w1);
+      if (wave > 1) {  // hand the partial accumulators to wave 1 (lane-major, 16 floats each)
+        float* pp = l1part + ((wave - 2) * 64 + lane) * 16;
 #pragma unroll
-      for (int rr = 0; rr < MDP_R; ++rr)
-        d2c[rr * LD + lane] = (rr < nvalid && h2c[rr * LH + lane] > 0.f) ? a.neg_inv_b * w3c : 0.f;
-      MDP_STAMPW(20);
-      __syncthreads();  // B3
-      __syncthreads();  // B4
-      __syncthreads();  // B5
-    } else {
-      gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
-      lds_signal(&rows_ready);
+        for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(pp + 4 * t) = acc[t];
+      }
       __syncthreads();  // B2
+      if (wave == 1) {
+        MDP_STAMPW(19);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[t] += *reinterpret_cast<const f32x4*>(l1part + lane * 16 + 4 * t);
+          acc[t] += *reinterpret_cast<const f32x4*>(l1part + (64 + lane) * 16 + 4 * t);
+        }
+        rf_acc<2>(acc, av, 8, MDP_ACT_DIM, w1b);
+        rf_store<true>(acc, b1, h1c, LH);
+      }
+      __syncthreads();  // B2b: h1c ready
+      critic_l2_tile(h1c, w2t, b2t, w3t, wave, nvalid, a.neg_inv_b, d2c, qpart);
+      if (wave == 1) MDP_STAMPW(20);
       __syncthreads();  // B3
       __syncthreads();  // B4
       __syncthreads();  // B5
@@ -562,6 +599,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);
     rdg_load(wa, P + na.t[2].off, 16 * tt + r, true);
     __syncthreads();  // B2
+    __syncthreads();  // B2b
     __syncthreads();  // B3
     if (tt == 0) MDP_STAMPW(21);
     dgrad_tile(d2c, wc, h1c, d1c, tt);
