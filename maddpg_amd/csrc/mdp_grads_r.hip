@@ -82,6 +82,43 @@ __device__ __forceinline__ void critic_l2_tile(const float* h1, const float (&w2
     if (r == 0) qpart[tt * MDP_R + row] = s;
   }
 }
+// rows 4 q .. 4 q + 3 of d2a = (dl W3a^T) o [h2a > 0] and their share of
+// dW3a = h2a^T dl (lane = hidden unit), one row quarter per wave 0..3
+__device__ __forceinline__ void d2a_rows(const float* h2a, const float* dl, const float (&w3a)[MDP_ACT_DIM], float* d2a,
+                                         float* gwpart, int q) {
+  const int lane = threadIdx.x & 63;
+  float gw[MDP_ACT_DIM] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = 4 * q + i;
+    const float h = h2a[rr * LH + lane];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MDP_ACT_DIM; ++k) {
+      const float d = dl[rr * 8 + k];
+      s = fmaf(d, w3a[k], s);
+      gw[k] = fmaf(h, d, gw[k]);
+    }
+    d2a[rr * LD + lane] = h > 0.f ? s : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < MDP_ACT_DIM; ++k) gwpart[(q * MDP_ACT_DIM + k) * 64 + lane] = gw[k];
+}
+// dW3a (sum of the four quarters, fixed order) and db3a = column sums of dl
+__device__ __forceinline__ void dw3a_store(const float* gwpart, const float* dl, float* dw3, float* db3) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < MDP_ACT_DIM; ++k) {
+    const float g = ((gwpart[k * 64 + lane] + gwpart[(MDP_ACT_DIM + k) * 64 + lane]) +
+                     gwpart[(2 * MDP_ACT_DIM + k) * 64 + lane]) + gwpart[(3 * MDP_ACT_DIM + k) * 64 + lane];
+    dw3[lane * MDP_ACT_DIM + k] = g;
+  }
+  if (lane < MDP_ACT_DIM) {
+    float s = 0.f;
+    for (int rr = 0; rr < MDP_R; ++rr) s += dl[rr * 8 + lane];
+    db3[lane] = s;
+  }
+}
 }  // namespace
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
@@ -404,6 +441,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   float* d2a = cv.take(MDP_R * LD);
   float* d1a = cv.take(MDP_R * LD);
   float* l1part = cv.take(2 * 64 * 16);  // critic L1 partial accumulators of waves 2, 3
+  float* gwpart = cv.take(4 * MDP_ACT_DIM * 64);  // dW3a partials of the four row quarters
   float* qpart = cv.take(4 * MDP_R);     // critic head partials of the four L2 column tiles
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -516,31 +554,11 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
         st[0] = s_q;
         st[1] = s_p;
       }
-      wave_sync();
-      // dW3a = h2a^T dl, db3a, d2a = (dl W3a^T) o [h2a > 0]   (lane = hidden unit)
-      {
-        float gw[MDP_ACT_DIM] = {0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int rr = 0; rr < MDP_R; ++rr) {
-          const float h = h2a[rr * LH + lane];
-          float s = 0.f;
-#pragma unroll
-          for (int k = 0; k < MDP_ACT_DIM; ++k) {
-            const float d = dl[rr * 8 + k];
-            s = fmaf(d, w3a[k], s);
-            gw[k] = fmaf(h, d, gw[k]);
-          }
-          d2a[rr * LD + lane] = h > 0.f ? s : 0.f;
-        }
-#pragma unroll
-        for (int k = 0; k < MDP_ACT_DIM; ++k) slab[na.t[4].off + lane * MDP_ACT_DIM + k] = gw[k];
-        if (lane < MDP_ACT_DIM) {
-          float s = 0.f;
-          for (int rr = 0; rr < MDP_R; ++rr) s += dl[rr * 8 + lane];
-          slab[na.t[5].off + lane] = s;
-        }
-      }
+      __syncthreads();  // B4b: dlogits ready
+      d2a_rows(h2a, dl, w3a, d2a, gwpart, 0);
       MDP_STAMP(24);
       __syncthreads();  // B5: d2a ready
+      dw3a_store(gwpart, dl, slab + na.t[4].off, slab + na.t[5].off);
     } else {
       // ---------------- critic (post-step weights) forward with a_i = the sample (maddpg.py:48-52)
       // waves 2, 3 gather their share of the replay rows first
@@ -581,8 +599,13 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       __syncthreads();  // B2b: h1c ready
       critic_l2_tile(h1c, w2t, b2t, w3t, wave, nvalid, a.neg_inv_b, d2c, qpart);
       if (wave == 1) MDP_STAMPW(20);
+      float w3a[MDP_ACT_DIM];
+#pragma unroll
+      for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
       __syncthreads();  // B3
       __syncthreads();  // B4
+      __syncthreads();  // B4b
+      d2a_rows(h2a, dl, w3a, d2a, gwpart, wave);
       __syncthreads();  // B5
     }
     // dW2a = h1a^T d2a (waves 0..3), db2a
@@ -605,6 +628,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     dgrad_tile(d2c, wc, h1c, d1c, tt);
     __syncthreads();  // B4
     if (tt == 0) MDP_STAMPW(22);
+    __syncthreads();  // B4b
     __syncthreads();  // B5
     if (tt == 0) MDP_STAMPW(25);
     dgrad_tile(d2a, wa, h1a, d1a, tt);

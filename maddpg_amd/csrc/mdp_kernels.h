@@ -184,7 +184,7 @@ inline int lds_critic_r_bytes(const Topo& t, int agent) {
 }
 inline int lds_actor_r_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, LD = 65;
-  return 4 * (mdp_r4(R * ldr) + 4 * R * 8 + R + 3 * R * LH + 4 * mdp_r4(R * LD) + 2 * 64 * 16 + 4 * R);
+  return 4 * (mdp_r4(R * ldr) + 4 * R * 8 + R + 3 * R * LH + 4 * mdp_r4(R * LD) + 2 * 64 * 16 + 4 * R + 4 * 5 * 64);
 }
 // the fast kernels hold every weight of a wave in registers: H = 64, at most 3
 // target actors, actor inputs <= 64, critic inputs <= 80, target-critic action part <= 20
