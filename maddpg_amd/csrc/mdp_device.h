@@ -147,6 +147,7 @@ __device__ __forceinline__ f32x4 mfma_chunk(f32x4 acc, const float (&w)[MDP_KC],
     const float v = A[r * lda + min(k, kmax)];
     x[s] = k < K ? v : 0.f;
   }
+  __builtin_amdgcn_sched_barrier(0);  // every A read ahead of the MFMA chain
 #pragma unroll
   for (int s = 0; s < MDP_KC; ++s) {
     if (c0 + 4 * s < K)  // wave-uniform
@@ -158,7 +159,7 @@ __device__ __forceinline__ f32x4 mfma_chunk(f32x4 acc, const float (&w)[MDP_KC],
 template <bool RELU>
 __device__ __forceinline__ void tile_fwd(const float* X, int ldx, int K, const float* __restrict__ W,
                                 const float* __restrict__ b, int N, float* Y, int ldy) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, kq = lane >> 4;
   for (int nt = wave; nt < (N >> 4); nt += MDP_NW) {
     const int col = nt * 16 + r;
@@ -188,7 +189,7 @@ __device__ __forceinline__ void tile_fwd(const float* X, int ldx, int K, const f
 // Rows >= K are not written.
 __device__ __forceinline__ void tile_wgrad(const float* X, int ldx, int K, const float* dY, int ldy, int N,
                                   float* __restrict__ dW) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, kq = lane >> 4;
   const int nmt = (K + 15) >> 4, nnt = N >> 4;
   for (int t = wave; t < nmt * nnt; t += MDP_NW) {
@@ -214,7 +215,7 @@ __device__ __forceinline__ void tile_wgrad(const float* X, int ldx, int K, const
 // (post-ReLU activations of the previous layer); K multiple of 16.
 __device__ __forceinline__ void tile_dgrad_relu(const float* dY, int ldy, int N, const float* __restrict__ W, int K,
                                        const float* Hin, int ldh, float* dX, int ldx) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 15, kq = lane >> 4;
   for (int nt = wave; nt < (K >> 4); nt += MDP_NW) {
     const int kk = nt * 16 + r;
@@ -236,6 +237,35 @@ __device__ __forceinline__ void tile_dgrad_relu(const float* dY, int ldy, int N,
       const float h = Hin[row * ldh + kk];
       dX[row * ldx + kk] = h > 0.f ? acc[i] : 0.f;
     }
+  }
+}
+
+// ONE wave: out[16][nout] = X[16][K] @ W[K][nout] + b for nout <= 16 as a single
+// MFMA column tile (column r = lane & 15): every weight of the lane is requested
+// up front (one memory round trip), then KS = K/4 dependent MFMAs.  Replaces
+// the VALU heads whose k-loop waited on one global load per iteration.
+template <int KS>
+__device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const float* __restrict__ W,
+                                          const float* __restrict__ b, int nout, float* out, int ldo) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int c = min(r, nout - 1), kmax = K - 1;
+  float w[KS], x[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + kq;
+    const float v = W[min(k, kmax) * nout + c];
+    w[s] = (r < nout && k < K) ? v : 0.f;
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) x[s] = X[r * ldx + min(4 * s + kq, kmax)];
+  const float bias = b[c];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+  if (r < nout) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(kq * 4 + i) * ldo + r] = acc[i] + bias;
   }
 }
 
@@ -825,7 +855,7 @@ __device__ __forceinline__ double sum16(double v) {
 // weight-gradient tiles over waves [w0, w0 + wn)
 __device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, const float* dY, int ldy, int N,
                                             float* __restrict__ dW, int w0, int wn) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wave < w0 || wave >= w0 + wn) return;
   const int r = lane & 15, kq = lane >> 4;
   const int nmt = (K + 15) >> 4, nnt = N >> 4;

@@ -1,29 +1,159 @@
-// mdp_grads.hip -- per-agent critic-step and actor-step gradient kernels (gfx950).
+// mdp_grads.hip -- per-agent critic-step and actor-step gradient kernels (gfx950),
+// general topology: H = 64 or 128, up to 8 agents, wide critic inputs (BASELINE
+// configs[4]: simple_tag N=6, H=128, B=4096).  The register-resident kernels
+// of mdp_grads_r.hip serve H = 64 with <= 3 target actors.
 //
 // One 512-thread workgroup (8 waves) owns 16 batch rows; the reduction over
-// the batch happens in k_reduce from per-workgroup partials (deterministic).
-//
-// Forward passes are WAVE-LOCAL: one wave runs a whole net (L1 -> L2 -> head)
-// with its H/16 column tiles' fp32-MFMA chains interleaved (wave_layer in
-// mdp_device.h) and only wave-scope LDS ordering between layers, so
-// independent nets (every agent's target actor and the critic) run
-// concurrently on different waves with no workgroup barrier between their
-// layers.  Workgroup barriers remain only where data crosses nets or rows
-// meet columns (weight gradients, spread over all waves).
+// the batch happens in k_reduce_apply from per-workgroup partials
+// (deterministic).  Every dense layer is spread over ALL waves as 16-column
+// MFMA tiles (fwd_tile / dgrad_tile_relu, weights streamed from L2 in 64-deep
+// chunks with the next chunk in flight); the tiles of independent nets of one
+// phase are dealt round-robin over the waves with no barrier between nets, so
+// a wave's load latency is covered by the other wave on its SIMD.  (The
+// earlier design ran one whole net per wave: at H = 128 a wave then waited on
+// ~600 MFMAs and every weight chunk in turn -- the target critic alone took
+// 21 us of a 98 us critic step.)
 //
 // k_critic_grad (maddpg.py:180-188):
-//   gather rows | waves: target actor j (+Gumbel a~_j), critic fwd  || barrier
-//   | wave 0: target critic -> fp64 TD target, loss, dL/dq             || barrier
-//   | dW3, db3, d2                                                     || barrier
-//   | wave 0: dh1 ; waves 1..7: dW2 ; db2                              || barrier
-//   | dW1, db1
+//   gather | L1 tiles of the target actors (+ critic) || L2 tiles || heads, Gumbel a~
+//   || target critic L1 || L2 || wave 0: head, fp64 TD, loss, dL/dq
+//   || dW3, db3, d2 || dh1 tiles + dW2 tiles || dW1, db1
 // k_actor_grad (maddpg.py:37-58):
-//   gather | wave 0: actor fwd, Gumbel a_i, critic(a_i) fwd, d2, dh1, da_i,
-//   softmax backward + reg -> dlogits                                  || barrier
-//   | dW3a, db3a, d2a || wave 0: d1a ; waves 1..7: dW2a || dW1a, db1a
+//   gather | actor L1 || L2 || head, Gumbel a_i, critic input || critic L1 || L2
+//   || head q, d2 || dh1c tiles || da, softmax backward + reg (wave 0)
+//   || dW3a, db3a, d2a || dh1a tiles + dW2a tiles || dW1a, db1a
 #include "mdp_device.h"
 #include "mdp_kernels.h"
 
+namespace {
+// Y[16][col tile nt] = act(X[16][K] @ W[K][N] + b), weights in 64-deep chunks, the next in flight
+template <bool RELU>
+__device__ __forceinline__ void fwd_tile(const float* X, int ldx, int K, const float* __restrict__ W,
+                                         const float* __restrict__ b, int N, float* Y, int ldy, int nt) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int col = nt * 16 + r;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float wa[MDP_KC], wb[MDP_KC];
+  load_wchunk(wa, W, N, col, 0, K, kq);
+  const float bias = b[col];
+  for (int c0 = 0; c0 < K; c0 += 4 * MDP_KC) {
+    const bool more = c0 + 4 * MDP_KC < K;
+    if (more) load_wchunk(wb, W, N, col, c0 + 4 * MDP_KC, K, kq);
+    acc = mfma_chunk(acc, wa, X, ldx, r, c0, K, kq);
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v = acc[i] + bias;
+    if (RELU) v = fmaxf(v, 0.f);
+    Y[(kq * 4 + i) * ldy + col] = v;
+  }
+}
+
+// A layer phase: the 16-column tiles of several dense layers Y = relu(X W + b)
+// (all N = H wide), dealt round-robin over the waves.  Each wave walks its
+// (tile, 64-deep chunk) items in order with the NEXT item's weight chunk in
+// flight -- across tile boundaries too, so the weight-load latency of a wave's
+// next tile hides behind the current tile's MFMAs.  Job q -> (X, K, W, b, Y)
+// comes from `job`, as LDS offsets and global pointers.
+struct TileJob {
+  int xoff, ldx, K;   // X = lds + xoff
+  const float* W;     // [K][N] global
+  const float* b;
+  int yoff;           // Y = lds + yoff (row stride ldy)
+};
+template <class JobFn>
+__device__ __forceinline__ void fwd_phase_pipelined(float* lds, int njobs, int N, int ldy, JobFn job) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+  const int r = lane & 15, kq = lane >> 4, ntl = N >> 4, total = njobs * ntl;
+  int t = wave;
+  if (t >= total) return;
+  TileJob j = job(t / ntl);
+  int col = (t % ntl) * 16 + r, c0 = 0;
+  float wa[MDP_KC], wb[MDP_KC];
+  load_wchunk(wa, j.W, N, col, 0, j.K, kq);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  while (true) {
+    int t2 = t, c2 = c0 + 4 * MDP_KC, col2 = col;
+    TileJob j2 = j;
+    if (c2 >= j.K) {  // next tile of this wave
+      t2 = t + nw;
+      c2 = 0;
+      if (t2 < total) {
+        j2 = job(t2 / ntl);
+        col2 = (t2 % ntl) * 16 + r;
+      }
+    }
+    const bool more = t2 < total;
+    if (more) load_wchunk(wb, j2.W, N, col2, c2, j2.K, kq);
+    acc = mfma_chunk(acc, wa, lds + j.xoff, j.ldx, r, c0, j.K, kq);
+    if (c0 + 4 * MDP_KC >= j.K) {  // tile done
+      const float bias = j.b[col];
+      float* Y = lds + j.yoff;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Y[(kq * 4 + i) * ldy + col] = fmaxf(acc[i] + bias, 0.f);
+      acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (!more) break;
+#pragma unroll
+    for (int s2 = 0; s2 < MDP_KC; ++s2) wa[s2] = wb[s2];
+    t = t2;
+    c0 = c2;
+    col = col2;
+    j = j2;
+  }
+}
+
+// dX[16][tile nt of K] = (dY[16][N] @ W^T) masked by Hin > 0, W[K][N] global
+__device__ __forceinline__ void dgrad_tile_relu(const float* dY, int ldy, int N, const float* __restrict__ W,
+                                                const float* Hin, int ldh, float* dX, int ldx, int nt) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int kk = nt * 16 + r;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float wa[MDP_KC], wb[MDP_KC];
+  load_wchunk_t(wa, W, N, kk, 0, N, kq, true);
+  for (int c0 = 0; c0 < N; c0 += 4 * MDP_KC) {
+    const bool more = c0 + 4 * MDP_KC < N;
+    if (more) load_wchunk_t(wb, W, N, kk, c0 + 4 * MDP_KC, N, kq, true);
+    acc = mfma_chunk(acc, wa, dY, ldy, r, c0, N, kq);
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = kq * 4 + i;
+    dX[row * ldx + kk] = Hin[row * ldh + kk] > 0.f ? acc[i] : 0.f;
+  }
+}
+
+// dW[K][N] tile t = (mt, nt) of X^T[K][16] @ dY[16][N], to global (stride N); rows >= K not written
+__device__ __forceinline__ void wgrad_tile(const float* X, int ldx, int K, const float* dY, int ldy, int N,
+                                           float* __restrict__ dW, int t) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int nnt = N >> 4, mt = t / nnt, nt = t - mt * nnt;
+  const int feat = mt * 16 + r;
+  const int fc = min(feat, K - 1);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r0 = 0; r0 < MDP_R; r0 += 4) {
+    const int row = r0 + kq;
+    const float xv = X[row * ldx + fc];
+    const float a = feat < K ? xv : 0.f;
+    const float g = dY[row * ldy + nt * 16 + r];
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = mt * 16 + kq * 4 + i;
+    if (k < K) dW[k * N + nt * 16 + r] = acc[i];
+  }
+}
+}  // namespace
 
 template <int H>
 __global__ __launch_bounds__(512) void k_critic_grad(CriticArgs a) {
@@ -43,7 +173,7 @@ __global__ __launch_bounds__(512) void k_critic_grad(CriticArgs a) {
   float* lg = cv.take((G + 1) * MDP_R * 8);
   float* dq = cv.take(MDP_R);
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = blockDim.x >> 6;
   const int r0 = blockIdx.x * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const bool lq = ag.local_q != 0;
@@ -69,53 +199,84 @@ __global__ __launch_bounds__(512) void k_critic_grad(CriticArgs a) {
   const int ldX = lq ? ldc : ldr;
   MDP_STAMP(1);
 
-  // one wave per net: target actors of the group (+ the critic forward with the first group)
+  // target actors of the group (+ the critic forward with the first group): each
+  // layer phase deals every net's 16-column tiles over all waves
   const int nact = lq ? 1 : T.n;
   for (int g0 = 0; g0 < nact; g0 += G) {
     const int ng = min(G, nact - g0);
     const int nj = ng + (g0 == 0 ? 1 : 0);
+    const int o_row = (int)(rowbuf - lds), o_xc = (int)(Xc - lds), o_ha = (int)(hA - lds), o_hb = (int)(hB - lds);
+    for (int layer = 0; layer < 2; ++layer) {
+      fwd_phase_pipelined(lds, nj, H, ldh, [&](int jb) {
+        const bool actor = jb < ng;
+        const ADesc& aj = T.ag[lq ? a.agent : g0 + jb];
+        const NDesc& net = actor ? aj.actor : nd;
+        const float* P = actor ? a.target : a.theta;
+        const int slot = (actor ? jb : G) * S;
+        TileJob j;
+        if (layer == 0) {
+          j.xoff = actor ? o_row + aj.nobs_off : o_xc;
+          j.ldx = actor ? ldr : ldX;
+          j.K = actor ? aj.obs_dim : ag.cin;
+          j.W = P + net.t[0].off;
+          j.b = P + net.t[1].off;
+          j.yoff = o_ha + slot;
+        } else {
+          j.xoff = o_ha + slot;
+          j.ldx = ldh;
+          j.K = H;
+          j.W = P + net.t[2].off;
+          j.b = P + net.t[3].off;
+          j.yoff = o_hb + slot;
+        }
+        return j;
+      });
+      __syncthreads();
+      if (g0 == 0) MDP_STAMP(6 + layer);
+    }
+    // heads: net jb on wave jb % nw, then the Gumbel-softmax target actions
     for (int jb = wave; jb < nj; jb += nw) {
       if (jb < ng) {
-        const int j = lq ? a.agent : g0 + jb;
-        const ADesc& aj = T.ag[j];
-        const float* P = a.target;
-        float* h1 = hA + jb * S;
-        float* h2 = hB + jb * S;
-        float* lgj = lg + jb * MDP_R * 8;
-        wave_layer<NT, true>(rowbuf + aj.nobs_off, ldr, aj.obs_dim, P + aj.actor.t[0].off, P + aj.actor.t[1].off, h1,
-                             ldh);
-        wave_layer<NT, true>(h1, ldh, H, P + aj.actor.t[2].off, P + aj.actor.t[3].off, h2, ldh);
-        wave_head(h2, ldh, H, P + aj.actor.t[4].off, P + aj.actor.t[5].off, MDP_ACT_DIM, lgj, 8);
-        if (lane < MDP_R) {  // Gumbel-softmax target action (distributions.py:264-266)
-          const int row = lane;
-          float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
-          if (a.u_tgt) {
-            for (int k = 0; k < MDP_ACT_DIM; ++k)
-              u[k] = row < nvalid ? a.u_tgt[((int64_t)j * a.B + r0 + row) * MDP_ACT_DIM + k] : 0.5f;
-          } else {
-            uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + row), u);
-          }
-          gumbel_softmax5(lgj + row * 8, u, act);
-          const int dst = lq ? ag.obs_dim : T.sum_obs + MDP_ACT_DIM * j;
-          for (int k = 0; k < MDP_ACT_DIM; ++k) xt[row * ldc + dst + k] = act[k];
-        }
+        const NDesc& an = T.ag[lq ? a.agent : g0 + jb].actor;
+        head_mfma<H / 4>(hB + jb * S, ldh, H, a.target + an.t[4].off, a.target + an.t[5].off, MDP_ACT_DIM,
+                         lg + jb * MDP_R * 8, 8);
       } else {
-        const float* P = a.theta;
-        wave_layer<NT, true>(Xc, ldX, ag.cin, P + nd.t[0].off, P + nd.t[1].off, h1c, ldh);
-        wave_layer<NT, true>(h1c, ldh, H, P + nd.t[2].off, P + nd.t[3].off, h2c, ldh);
-        wave_head(h2c, ldh, H, P + nd.t[4].off, P + nd.t[5].off, 1, qv, 8);
+        head_mfma<H / 4>(h2c, ldh, H, a.theta + nd.t[4].off, a.theta + nd.t[5].off, 1, qv, 8);
       }
+    }
+    __syncthreads();
+    if (g0 == 0) MDP_STAMP(8);
+    for (int e = tid; e < ng * MDP_R; e += blockDim.x) {  // distributions.py:264-266
+      const int jb = e / MDP_R, row = e - jb * MDP_R;
+      const int j = lq ? a.agent : g0 + jb;
+      float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
+      if (a.u_tgt) {
+        for (int k = 0; k < MDP_ACT_DIM; ++k)
+          u[k] = row < nvalid ? a.u_tgt[((int64_t)j * a.B + r0 + row) * MDP_ACT_DIM + k] : 0.5f;
+      } else {
+        uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + row), u);
+      }
+      gumbel_softmax5(lg + jb * MDP_R * 8 + row * 8, u, act);
+      const int dst = lq ? ag.obs_dim : T.sum_obs + MDP_ACT_DIM * j;
+      for (int k = 0; k < MDP_ACT_DIM; ++k) xt[row * ldc + dst + k] = act[k];
     }
     __syncthreads();
   }
   MDP_STAMP(2);
 
-  // wave 0: target critic Q'(o', a~), fp64 TD target (maddpg.py:186), loss partials, dL/dq = 2(q-y)/B
+  // target critic Q'(o', a~) over all waves; wave 0: head, fp64 TD target
+  // (maddpg.py:186), loss partials, dL/dq = 2(q-y)/B
+  {
+    const float* P = a.target;
+    for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(xt, ldc, ag.cin, P + nd.t[0].off, P + nd.t[1].off, H, hA, ldh, nt);
+    __syncthreads();
+    for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(hA, ldh, H, P + nd.t[2].off, P + nd.t[3].off, H, hB, ldh, nt);
+    __syncthreads();
+  }
   if (wave == 0) {
     const float* P = a.target;
-    wave_layer<NT, true>(xt, ldc, ag.cin, P + nd.t[0].off, P + nd.t[1].off, hA, ldh);
-    wave_layer<NT, true>(hA, ldh, H, P + nd.t[2].off, P + nd.t[3].off, hB, ldh);
-    wave_head(hB, ldh, H, P + nd.t[4].off, P + nd.t[5].off, 1, lg, 8);
+    head_mfma<H / 4>(hB, ldh, H, P + nd.t[4].off, P + nd.t[5].off, 1, lg, 8);
+    wave_sync();
     double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;
     float g = 0.f;
     if (lane < nvalid) {
@@ -169,8 +330,11 @@ __global__ __launch_bounds__(512) void k_critic_grad(CriticArgs a) {
   }
   __syncthreads();
   MDP_STAMP(4);
-  if (wave == 0) wave_dgrad<NT>(d2, ldh, H, a.theta + nd.t[2].off, h1c, ldh, d1, ldh);
-  wgrad_waves(h1c, ldh, H, d2, ldh, H, slab + nd.t[2].off, 1, nw - 1);
+  // dh1 tiles then dW2 tiles, dealt over all waves
+  for (int t = wave; t < NT + NT * NT; t += nw) {
+    if (t < NT) dgrad_tile_relu(d2, ldh, H, a.theta + nd.t[2].off, h1c, ldh, d1, ldh, t);
+    else wgrad_tile(h1c, ldh, H, d2, ldh, H, slab + nd.t[2].off, t - NT);
+  }
   colsum16(d2, ldh, H, slab + nd.t[3].off);
   __syncthreads();
   wgrad_waves(Xc, ldX, ag.cin, d1, ldh, H, slab + nd.t[0].off, 0, nw);
@@ -201,7 +365,7 @@ __global__ __launch_bounds__(512) void k_actor_grad(ActorArgs a) {
   float* dl = cv.take(MDP_R * 8);
   float* qv = cv.take(MDP_R * 8);
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = blockDim.x >> 6;
   const int r0 = blockIdx.x * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const bool lq = ag.local_q != 0;
@@ -209,23 +373,27 @@ __global__ __launch_bounds__(512) void k_actor_grad(ActorArgs a) {
   const NDesc& na = ag.actor;
   const NDesc& nc = ag.critic;
   const float* P = a.theta;
+  const int cin = ag.cin;
 
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
   __syncthreads();
+  // actor forward on obs_i -> logits p (maddpg.py:39)
+  for (int nt = wave; nt < NT; nt += nw)
+    fwd_tile<true>(rowbuf + ag.obs_off, ldr, ag.obs_dim, P + na.t[0].off, P + na.t[1].off, H, h1a, ldh, nt);
+  // critic input with act_input_n[i] = the sample (maddpg.py:48-52): the replay part now
+  for (int e = tid; e < MDP_R * cin; e += blockDim.x) {
+    const int r = e / cin, c = e - r * cin;
+    const int src = lq ? (c < ag.obs_dim ? ag.obs_off + c : ag.act_off + c - ag.obs_dim) : c;
+    x[r * ldc + c] = rowbuf[r * ldr + src];
+  }
+  __syncthreads();
+  for (int nt = wave; nt < NT; nt += nw)
+    fwd_tile<true>(h1a, ldh, H, P + na.t[2].off, P + na.t[3].off, H, h2a, ldh, nt);
+  __syncthreads();
   if (wave == 0) {
-    // actor forward on obs_i -> logits p (maddpg.py:39), fresh Gumbel sample (:49)
-    wave_layer<NT, true>(rowbuf + ag.obs_off, ldr, ag.obs_dim, P + na.t[0].off, P + na.t[1].off, h1a, ldh);
-    wave_layer<NT, true>(h1a, ldh, H, P + na.t[2].off, P + na.t[3].off, h2a, ldh);
-    wave_head(h2a, ldh, H, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM, lg, 8);
-    // critic input with act_input_n[i] = the sample (maddpg.py:48-52)
-    const int cin = ag.cin;
-    for (int e = lane; e < MDP_R * cin; e += 64) {
-      const int r = e / cin, c = e - r * cin;
-      const int src = lq ? (c < ag.obs_dim ? ag.obs_off + c : ag.act_off + c - ag.obs_dim) : c;
-      x[r * ldc + c] = rowbuf[r * ldr + src];
-    }
+    head_mfma<H / 4>(h2a, ldh, H, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM, lg, 8);
     wave_sync();
-    if (lane < MDP_R) {
+    if (lane < MDP_R) {  // fresh Gumbel sample (maddpg.py:49)
       float u[MDP_ACT_DIM];
       if (a.u_act) {
         for (int k = 0; k < MDP_ACT_DIM; ++k)
@@ -236,19 +404,26 @@ __global__ __launch_bounds__(512) void k_actor_grad(ActorArgs a) {
       gumbel_softmax5(lg + lane * 8, u, av + lane * 8);
       for (int k = 0; k < MDP_ACT_DIM; ++k) x[lane * ldc + ag.a_in_off + k] = av[lane * 8 + k];
     }
-    wave_sync();
-    // critic (post-step weights) forward, q for the loss value
-    wave_layer<NT, true>(x, ldc, cin, P + nc.t[0].off, P + nc.t[1].off, h1c, ldh);
-    wave_layer<NT, true>(h1c, ldh, H, P + nc.t[2].off, P + nc.t[3].off, h2c, ldh);
-    wave_head(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
-    // dL/dq = -1/B ; d2 = dq * W3c masked by h2c > 0 ; dh1 = d2 @ W2c^T masked by h1c > 0
-    const float* W3c = P + nc.t[4].off;
-    for (int e = lane; e < MDP_R * H; e += 64) {
-      const int r = e / H, h = e - r * H;
-      d2[r * ldh + h] = (r < nvalid && h2c[r * ldh + h] > 0.f) ? a.neg_inv_b * W3c[h] : 0.f;
-    }
-    wave_sync();
-    wave_dgrad<NT>(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh);
+  }
+  __syncthreads();
+  // critic (post-step weights) forward
+  for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(x, ldc, cin, P + nc.t[0].off, P + nc.t[1].off, H, h1c, ldh, nt);
+  __syncthreads();
+  for (int nt = wave; nt < NT; nt += nw)
+    fwd_tile<true>(h1c, ldh, H, P + nc.t[2].off, P + nc.t[3].off, H, h2c, ldh, nt);
+  __syncthreads();
+  // q (loss value, wave 0) ; dL/dq = -1/B ; d2 = dq * W3c masked by h2c > 0
+  if (wave == 0) head_mfma<H / 4>(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
+  const float* W3c = P + nc.t[4].off;
+  for (int e = tid; e < MDP_R * H; e += blockDim.x) {
+    const int r = e / H, h = e - r * H;
+    d2[r * ldh + h] = (r < nvalid && h2c[r * ldh + h] > 0.f) ? a.neg_inv_b * W3c[h] : 0.f;
+  }
+  __syncthreads();
+  // dh1c = d2 @ W2c^T masked by h1c > 0
+  for (int nt = wave; nt < NT; nt += nw) dgrad_tile_relu(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh, nt);
+  __syncthreads();
+  if (wave == 0) {
     // da[r][k] = sum_h d1[r][h] * W1c[a_in_off + k][h]   (only the a_i input columns)
     {
       const float* W1c = P + nc.t[0].off + (int64_t)ag.a_in_off * H;
@@ -310,8 +485,11 @@ __global__ __launch_bounds__(512) void k_actor_grad(ActorArgs a) {
     d2[r * ldh + h] = h2a[r * ldh + h] > 0.f ? s : 0.f;
   }
   __syncthreads();
-  if (wave == 0) wave_dgrad<NT>(d2, ldh, H, P + na.t[2].off, h1a, ldh, d1, ldh);
-  wgrad_waves(h1a, ldh, H, d2, ldh, H, slab + na.t[2].off, 1, nw - 1);
+  // dh1a tiles then dW2a tiles, dealt over all waves
+  for (int t = wave; t < NT + NT * NT; t += nw) {
+    if (t < NT) dgrad_tile_relu(d2, ldh, H, P + na.t[2].off, h1a, ldh, d1, ldh, t);
+    else wgrad_tile(h1a, ldh, H, d2, ldh, H, slab + na.t[2].off, t - NT);
+  }
   colsum16(d2, ldh, H, slab + na.t[3].off);
   __syncthreads();
   wgrad_waves(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1, ldh, H, slab + na.t[0].off, 0, nw);

@@ -118,7 +118,7 @@ __device__ inline void mlp_fwd_tile(const float* X, int ldx, int K, const float*
   __syncthreads();
   tile_fwd<true>(h1, ldh, H, P + nd.t[2].off, P + nd.t[3].off, H, h2, ldh);
   __syncthreads();
-  tile_head(h2, ldh, H, P + nd.t[4].off, P + nd.t[5].off, nd.out, out, ldo);
+  if (threadIdx.x < 64) head_mfma<H / 4>(h2, ldh, H, P + nd.t[4].off, P + nd.t[5].off, nd.out, out, ldo);
   __syncthreads();
 }
 

@@ -16,12 +16,16 @@ from maddpg_amd import _lib  # noqa: E402
 from maddpg_amd.engine import Engine  # noqa: E402
 
 assert "stamps" in _lib.LIB_PATH
-eng = Engine([18, 18, 18], batch_size=1024, capacity=30000)
-eng.add_rows(torch.rand(30000, eng.row_stride))
+# MDP_STAMP_CFG=tag6: BASELINE configs[4] (simple_tag 4+2 agents, H=128, B=4096; general kernels)
+if os.environ.get("MDP_STAMP_CFG") == "tag6":
+    eng = Engine([22, 22, 22, 22, 20, 20], num_units=128, batch_size=4096, capacity=120000)
+else:
+    eng = Engine([18, 18, 18], batch_size=1024, capacity=30000)
+eng.add_rows(torch.rand(eng.capacity, eng.row_stride))
 eng.init_params(0)
 eng.seed_py_random(0)
 lib = _lib.load()
-fast = os.environ.get("MDP_GENERAL_GRADS") != "1"
+fast = eng.lib.mdp_grad_variant(eng.h, 0) == 1
 fn = lib.mdp_debug_stamps_r if fast else lib.mdp_debug_stamps
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 for it in range(5):
@@ -31,9 +35,13 @@ buf = (ctypes.c_ulonglong * 64)()
 fn(buf, 64)
 st = np.array(buf[:], dtype=np.int64)
 if not fast:
-    names = {0: "start", 1: "gather+copies", 2: "tgt actors+critic fwd", 3: "tgt critic", 4: "TD,stats,dW3,d2",
-             5: "dh1,dW2,dW1"}
-    seq = [(0, 6)]
+    names = {0: "start", 1: "gather+copies", 6: "L1 phase (group 0)", 7: "L2 phase", 8: "heads",
+             2: "Gumbel (+ later groups)", 3: "tgt critic", 4: "TD,stats,dW3,d2", 5: "dh1,dW2,dW1"}
+    prev = st[0]
+    for i in (1, 6, 7, 8, 2, 3, 4, 5):
+        print(f"{names[i]:>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us  (t={(st[i] - st[0]) * 10 / 1000:6.2f})")
+        prev = st[i]
+    seq = []
 else:
     names = {0: "start", 1: "B1 gather+weights (w0)", 2: "tgt actor fwd+gumbel (w0)", 3: "critic L1+L2 (w3)",
              4: "B2 (w4)", 5: "tgt L1 a~ part | B3 (w4)", 6: "tgt L2 tile | B4 (w4)", 7: "head, TD, d2 (w4)",
