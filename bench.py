@@ -325,7 +325,7 @@ def main():
             "rounds_per_sec": round(rounds / dt, 3),
             "rollout_only_env_steps_per_sec": round(rollout_only, 3),
             "update_rounds": rounds,
-            "dp": ("native-rccl" if getattr(r, "native_dp", False) else "torch.distributed") if world > 1 else None,
+            "dp": r.dp_kind if world > 1 else None,
             "kernel_pass": {"steps": prof_steps, "event_pair_overhead_ms": round(ev_ms, 5),
                             "per_kind_ms_per_launch": {k: round(v[0] / v[1] - ev_ms, 5) for k, v in per_kind.items()
                                                        if v[1]},

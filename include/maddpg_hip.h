@@ -177,6 +177,26 @@ int mdp_train_step(mdp_handle* h, int32_t rounds);
  * the environment captures them in the step graph). RCCL is dlopen'ed. */
 int mdp_dp_unique_id(uint8_t* out128);
 int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank);
+
+/* ---- direct xGMI gradient exchange (alternative to mdp_dp_init) ---------
+ * Same semantics as the RCCL path (sum over ranks in rank order, x 1/G, every
+ * replica bit-identical), but the exchange runs INSIDE the fused optimizer
+ * kernel: each 256-parameter chunk workgroup stores its reduced chunk straight
+ * into every peer's IPC-mapped buffer over xGMI, raises a per-chunk flag and
+ * sums the world's chunks -- no collective launch, so a data-parallel update
+ * has the single-GPU launch count (4 per agent strict, 3 per round
+ * throughput).  Handshake (every rank, in order):
+ *   open(world, rank) -> its 64-byte IPC handle; the caller all-gathers the
+ *   handles; connect(handles[world][64]); probe() exchanges a known pattern
+ *   (0 = every value arrived; fails after 10 s without a peer); the caller
+ *   agrees on success across ranks, then enable() -- or close() everywhere and
+ *   fall back to mdp_dp_init.  world 2..8. */
+#define MDP_XGMI_HANDLE_BYTES 64
+int mdp_dp_xgmi_open(mdp_handle* h, int32_t world, int32_t rank, uint8_t* handle_out);
+int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles);
+int mdp_dp_xgmi_probe(mdp_handle* h, int32_t* mismatches);
+int mdp_dp_xgmi_enable(mdp_handle* h);
+int mdp_dp_xgmi_close(mdp_handle* h);
 /* phase entry points for data parallelism (grad -> all-reduce -> apply) */
 int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev);
 int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev);

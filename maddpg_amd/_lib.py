@@ -106,6 +106,11 @@ SIGNATURES = {
     "mdp_dp_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "mdp_grad_variant": (ctypes.c_int, [_P, _I32]),
     "mdp_dp_init": (ctypes.c_int, [_P, ctypes.c_char_p, _I32, _I32]),
+    "mdp_dp_xgmi_open": (ctypes.c_int, [_P, _I32, _I32, ctypes.c_char_p]),
+    "mdp_dp_xgmi_connect": (ctypes.c_int, [_P, ctypes.c_char_p]),
+    "mdp_dp_xgmi_probe": (ctypes.c_int, [_P, _I32P]),
+    "mdp_dp_xgmi_enable": (ctypes.c_int, [_P]),
+    "mdp_dp_xgmi_close": (ctypes.c_int, [_P]),
     "mdp_critic_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_actor_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_reduce_grad": (ctypes.c_int, [_P, _I32, _I32]),

@@ -291,6 +291,16 @@ struct mdp_handle {
   FusedApplyArgs* tp_list = nullptr;  // device copy of the 2n optimizer steps (throughput mode)
   RaBatch tp_batch;                   // single GPU: reduce + step
   RaBatch tp_reduce, tp_step;         // data parallel: reduce pass, all-reduce, step pass (x 1/G)
+  RaBatch tp_xchg;                    // data parallel over xGMI: reduce + exchange + step (x 1/G)
+  // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
+  // the device descriptor of every rank's buffer mapped here
+  float* xbuf = nullptr;
+  int x_world = 0, x_rank = 0;
+  std::vector<void*> x_opened;        // peer buffers opened with hipIpcOpenMemHandle
+  XchgDesc* xd_dev = nullptr;
+  uint32_t* x_probe = nullptr;        // [0] mismatches, [1] fault of the connection probe
+  uint32_t x_probe_ep = 0;
+  bool p2p = false;
 };
 
 namespace {
@@ -535,11 +545,39 @@ FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net) {
   f.done_ctr = f.sync_ctr + 6 * 32;
   f.sync_part = h->ra_part + (int64_t)g * 6 * MDP_RA_MAXCH;
   f.phase = 0;
+  f.xd = nullptr;
+  f.net_id = g;
+  f.xstep = nullptr;
   return f;
 }
 
+// phase 3: reduce + xGMI exchange with every rank + step x 1/G (one launch)
+void set_xchg(mdp_handle* h, FusedApplyArgs& f, int agent, int net) {
+  f.phase = 3;
+  f.ap.scale = 1.0f / (float)h->dp_world;
+  f.xd = h->xd_dev;
+  f.net_id = 2 * agent + net;
+  f.xstep = h->ctl->xstep + f.net_id;
+}
+
+void xgmi_release(mdp_handle* h) {
+  for (void* p : h->x_opened)
+    if (p) (void)hipIpcCloseMemHandle(p);
+  h->x_opened.clear();
+  if (h->xd_dev) (void)hipFree(h->xd_dev);
+  if (h->x_probe) (void)hipFree(h->x_probe);
+  if (h->xbuf) (void)hipFree(h->xbuf);
+  h->xd_dev = nullptr;
+  h->x_probe = nullptr;
+  h->xbuf = nullptr;
+  h->p2p = false;
+  h->x_world = 0;
+  h->x_rank = 0;
+}
+
 int do_reduce_apply(mdp_handle* h, int agent, int net) {
-  const FusedApplyArgs f = fused_args_for(h, agent, net);
+  FusedApplyArgs f = fused_args_for(h, agent, net);
+  if (h->p2p) set_xchg(h, f, agent, net);
   ProfScope p(h, MDP_K_REDUCE_APPLY);
   HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
   return 0;
@@ -618,6 +656,12 @@ int dp_allreduce_all(mdp_handle* h) {
 int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out) {
   const float scale = 1.0f / (float)h->dp_world;
   int rc;
+  if (h->p2p) {  // the exchange lives inside the optimizer launch: same 4 launches as one GPU
+    if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out))) return rc;
+    if ((rc = do_reduce_apply(h, agent, 1))) return rc;
+    if ((rc = do_actor_grad(h, agent, idx, nullptr))) return rc;
+    return do_reduce_apply(h, agent, 0);
+  }
   if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out))) return rc;
   if ((rc = do_reduce(h, agent, 1))) return rc;
   if ((rc = dp_allreduce(h, agent, 1))) return rc;
@@ -631,7 +675,7 @@ int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out) 
 // pf_out: the critic kernel also draws the next round's indices there (fast path only)
 int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act,
               int32_t* pf_out = nullptr) {
-  if (h->comm && !u_tgt && !u_act) return do_update_dp(h, agent, idx, pf_out);
+  if ((h->comm || h->p2p) && !u_tgt && !u_act) return do_update_dp(h, agent, idx, pf_out);
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
   if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out))) return rc;
@@ -678,8 +722,9 @@ FusedApplyArgs tp_args(mdp_handle* h, int agent, int net) {
   return f;
 }
 
-// three device lists of the 2n steps: [0, 2n) fused (single GPU), [2n, 4n)
-// reduce-only, [4n, 6n) step from the all-reduced grad[] scaled by 1/G
+// four device lists of the 2n steps: [0, 2n) fused (single GPU), [2n, 4n)
+// reduce-only, [4n, 6n) step from the all-reduced grad[] scaled by 1/G,
+// [6n, 8n) reduce + xGMI exchange + step (phase 3)
 int tp_setup(mdp_handle* h) {
   if (h->tp_list) {
     (void)hipFree(h->tp_list);
@@ -687,8 +732,8 @@ int tp_setup(mdp_handle* h) {
   }
   const int n = h->cfg.n_agents;
   std::vector<FusedApplyArgs> list;
-  RaBatch* rbs[3] = {&h->tp_batch, &h->tp_reduce, &h->tp_step};
-  for (int ph = 0; ph < 3; ++ph) {
+  RaBatch* rbs[4] = {&h->tp_batch, &h->tp_reduce, &h->tp_step, &h->tp_xchg};
+  for (int ph = 0; ph < 4; ++ph) {
     RaBatch& rb = *rbs[ph];
     rb.count = 2 * n;
     rb.wg_start[0] = 0;
@@ -697,6 +742,10 @@ int tp_setup(mdp_handle* h) {
         FusedApplyArgs f = tp_args(h, i, net);
         f.phase = ph;
         if (ph == 2) f.ap.scale = 1.0f / (float)h->dp_world;
+        if (ph == 3) {
+          if (h->p2p) set_xchg(h, f, i, net);
+          else f.phase = 0;  // unused list
+        }
         list.push_back(f);
         const int q = 2 * i + (1 - net);
         rb.wg_start[q + 1] = rb.wg_start[q] + mdp_ra_grid(f);
@@ -704,7 +753,7 @@ int tp_setup(mdp_handle* h) {
   }
   HIPCHK(h, hipMalloc((void**)&h->tp_list, sizeof(FusedApplyArgs) * list.size()));
   HIPCHK(h, hipMemcpy(h->tp_list, list.data(), sizeof(FusedApplyArgs) * list.size(), hipMemcpyHostToDevice));
-  for (int ph = 0; ph < 3; ++ph) rbs[ph]->list = h->tp_list + (int64_t)ph * 2 * n;
+  for (int ph = 0; ph < 4; ++ph) rbs[ph]->list = h->tp_list + (int64_t)ph * 2 * n;
   return 0;
 }
 
@@ -764,6 +813,11 @@ int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const flo
     a.slab_agent_stride = nwg * h->L.slab_a;
     ProfScope p(h, MDP_K_ACTOR_GRAD);
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
+  }
+  if (h->p2p) {  // data parallel over xGMI: reduce + exchange + step of every net, one launch
+    ProfScope p(h, MDP_K_REDUCE_APPLY);
+    HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_xchg, h->stream));
+    return 0;
   }
   if (h->comm) {  // data parallel: ONE all-reduce of every net's gradient per round
     {
@@ -902,6 +956,7 @@ int mdp_destroy(mdp_handle* h) {
     for (auto e : h->ev[k]) (void)hipEventDestroy(e);
   if (h->round_exec) (void)hipGraphExecDestroy(h->round_exec);
   if (h->comm) (void)rccl().destroy(h->comm);
+  xgmi_release(h);
   for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
   if (h->round_graph) (void)hipGraphDestroy(h->round_graph);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -914,6 +969,11 @@ void* mdp_stream(mdp_handle* h) { return h ? (void*)h->stream : nullptr; }
 
 int mdp_synchronize(mdp_handle* h) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  uint32_t fault = 0;
+  HIPCHK(h, hipMemcpy(&fault, &h->ctl->fault, sizeof(fault), hipMemcpyDeviceToHost));
+  if (fault == 1) return fail(h, "device fault: a tensor-norm handshake timed out (k_reduce_apply)");
+  if (fault == 2) return fail(h, "device fault: a data-parallel peer did not reach the xGMI exchange within 10 s");
+  if (fault) return fail(h, "device fault");
   return 0;
 }
 
@@ -1216,6 +1276,7 @@ int mdp_dp_unique_id(uint8_t* out128) {
 int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank) {
   if (h && h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
   if (!h || !id128) return -1;
+  if (h->p2p || h->xbuf) return fail(h, "mdp_dp_init: the xGMI exchange is already set up");
   if (!rccl().ok) return fail(h, "librccl.so.1 could not be loaded");
   if (world < 1 || rank < 0 || rank >= world) return fail(h, "mdp_dp_init: bad world/rank");
   if (h->comm) return fail(h, "mdp_dp_init: already initialised");
@@ -1242,6 +1303,101 @@ int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank
     (void)hipGraphDestroy(h->round_graph);
     h->round_graph = nullptr;
   }
+  return 0;
+}
+
+static void drop_graphs(mdp_handle* h);
+
+int mdp_dp_xgmi_open(mdp_handle* h, int32_t world, int32_t rank, uint8_t* handle_out) {
+  if (!h || !handle_out) return -1;
+  if (h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
+  if (h->comm) return fail(h, "mdp_dp_xgmi_open: an RCCL communicator is already set up");
+  if (h->xbuf) return fail(h, "mdp_dp_xgmi_open: already open");
+  if (world < 2 || world > MDP_XCH_MAXW || rank < 0 || rank >= world)
+    return fail(h, "mdp_dp_xgmi_open: world must be 2..8 and 0 <= rank < world");
+  if (h->general_grads || !h->fused_apply) return fail(h, "the xGMI exchange needs the fused optimizer kernel");
+  for (int i = 0; i < h->cfg.n_agents; ++i)
+    for (int net = 0; net < 2; ++net) {
+      if (!reduce_apply_ok(h, i, net)) return fail(h, "the xGMI exchange needs the fused optimizer kernel");
+      if (fused_args_for(h, i, net).rblk[6] > MDP_XCH_FCH) return fail(h, "net too large for the exchange flags");
+    }
+  HIPCHK(h, hipSetDevice(h->device));
+  const int64_t bytes = mdp_xch_bytes(world, h->L.PT);
+  void* p = nullptr;
+  HIPCHK(h, hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached));
+  h->xbuf = (float*)p;
+  HIPCHK(h, hipMemset(p, 0, (size_t)bytes));
+  HIPCHK(h, hipMalloc((void**)&h->x_probe, 2 * sizeof(uint32_t)));
+  HIPCHK(h, hipDeviceSynchronize());
+  hipIpcMemHandle_t mh;
+  HIPCHK(h, hipIpcGetMemHandle(&mh, p));
+  static_assert(sizeof(mh) == MDP_XGMI_HANDLE_BYTES, "IPC handle size");
+  std::memcpy(handle_out, &mh, sizeof(mh));
+  h->x_world = world;
+  h->x_rank = rank;
+  return 0;
+}
+
+int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles) {
+  if (!h || !handles) return -1;
+  if (!h->xbuf) return fail(h, "mdp_dp_xgmi_connect: call mdp_dp_xgmi_open first");
+  if (!h->x_opened.empty()) return fail(h, "mdp_dp_xgmi_connect: already connected");
+  const int W = h->x_world, r = h->x_rank;
+  XchgDesc xd;
+  std::memset(&xd, 0, sizeof(xd));
+  xd.world = W;
+  xd.rank = r;
+  xd.pt = h->L.PT;
+  h->x_opened.assign(W, nullptr);
+  for (int q = 0; q < W; ++q) {
+    void* base = h->xbuf;
+    if (q != r) {
+      hipIpcMemHandle_t mh;
+      std::memcpy(&mh, handles + (int64_t)q * MDP_XGMI_HANDLE_BYTES, sizeof(mh));
+      const hipError_t e = hipIpcOpenMemHandle(&base, mh, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) return fail(h, "hipIpcOpenMemHandle", e);
+      h->x_opened[q] = base;
+    }
+    xd.data[q] = (float*)base;
+    xd.flags[q] = (uint32_t*)((char*)base + mdp_xch_data_bytes(W, h->L.PT));
+  }
+  HIPCHK(h, hipMalloc((void**)&h->xd_dev, sizeof(XchgDesc)));
+  HIPCHK(h, hipMemcpy(h->xd_dev, &xd, sizeof(XchgDesc), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int mdp_dp_xgmi_probe(mdp_handle* h, int32_t* mismatches) {
+  if (!h || !h->xd_dev) return fail(h, "mdp_dp_xgmi_probe: not connected");
+  const int nchunk = (int)std::min<int64_t>(8, h->L.PT / MDP_RA_CHUNK);
+  if (nchunk < 1) return fail(h, "mdp_dp_xgmi_probe: parameter space too small");
+  HIPCHK(h, hipMemsetAsync(h->x_probe, 0, 2 * sizeof(uint32_t), h->stream));
+  for (int k = 0; k < 4; ++k)  // both slots, each reused once
+    HIPCHK(h, mdp_launch_xchg_probe(h->xd_dev, ++h->x_probe_ep, nchunk, h->x_probe, h->x_probe + 1, h->stream));
+  uint32_t res[2] = {0, 0};
+  HIPCHK(h, hipMemcpyAsync(res, h->x_probe, sizeof(res), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (mismatches) *mismatches = (int32_t)res[0];
+  if (res[1]) return fail(h, "mdp_dp_xgmi_probe: a peer did not reach the exchange within 10 s");
+  if (res[0]) return fail(h, "mdp_dp_xgmi_probe: exchanged values differ from the expected world sum");
+  return 0;
+}
+
+int mdp_dp_xgmi_enable(mdp_handle* h) {
+  if (!h || !h->xd_dev) return fail(h, "mdp_dp_xgmi_enable: not connected");
+  if (h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->p2p = true;
+  h->dp_world = h->x_world;
+  drop_graphs(h);  // graphs captured without the exchange
+  return 0;
+}
+
+int mdp_dp_xgmi_close(mdp_handle* h) {
+  if (!h) return -1;
+  if (h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
+  xgmi_release(h);
+  if (!h->comm) h->dp_world = 1;
+  drop_graphs(h);
   return 0;
 }
 
@@ -1427,7 +1583,9 @@ int mdp_train_step(mdp_handle* h, int32_t rounds) {
   // the index kernels read the ring length the rollout leaves (device Ctl); the
   // host mirror moves first so the empty-buffer guard sees the same state
   advance_ring_mirror(h);
-  const bool no_graph = h->comm && !h->dp_graphs;  // collectives launched eagerly unless asked
+  // RCCL collectives are launched eagerly unless asked; the xGMI exchange is
+  // inside the optimizer kernels, so those steps are always captured
+  const bool no_graph = h->comm && !h->dp_graphs;
   if (!h->graphs || no_graph || any_prof(h) || h->eager_steps < 1 || rounds == 0) {
     if (rounds > 0) ++h->eager_steps;  // first training step eager (one-time kernel attribute setup)
     rc = step_launches(h, rounds);

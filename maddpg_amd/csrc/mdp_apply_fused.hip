@@ -1,7 +1,9 @@
 // mdp_apply_fused.hip -- one launch for the batch reduction + optimizer step
-// of one net (single-GPU path; with world_size > 1 the reduced gradient must
-// be materialised for the RCCL all-reduce, so k_reduce -> all-reduce -> k_apply
-// stay separate).
+// of one net.  Single GPU: phase 0.  Data parallel over RCCL: phase 1 (reduce
+// into grad[]) -> ncclAllReduce -> phase 2 (step).  Data parallel over the
+// direct xGMI exchange: phase 3, still ONE launch -- each chunk workgroup
+// pushes its reduced chunk to every peer and sums the world's chunks in rank
+// order before the clip/Adam below (xchg_chunk).
 //
 // Workgroup (tensor t, chunk c) of 256 parameters, 1024 threads: 16 groups of
 // 64 threads each sum a quarter-ish of the per-workgroup partial gradients of
@@ -31,7 +33,89 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
 __device__ __forceinline__ double ld_agent(const double* p) {
   return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// a peer that has not arrived after this long (s_memrealtime runs at 100 MHz)
+// is taken to be gone: the wait records Ctl::fault = 2 and gives up, and later
+// exchanges skip their waits (the host reports the fault at the next sync)
+constexpr uint64_t kXchgTimeoutTicks = 10ull * 100000000ull;
+
+// system-scope (cache-bypassing) load of 4 floats a peer wrote into our buffer
+__device__ __forceinline__ f32x4 ld_sys4(const float* p) {
+  uint32_t* u = reinterpret_cast<uint32_t*>(const_cast<float*>(p));
+  f32x4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    v[j] = __uint_as_float(__hip_atomic_load(u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  return v;
+}
+
+// The xGMI exchange of one 256-parameter chunk (flag row `row`, chunk b),
+// run by ONE wave.  g: this rank's reduced chunk (lane = 4 parameters at
+// param-space offset i0); returns the sum over ranks in rank order (identical
+// on every rank).  The exchange buffers are uncached device memory: the
+// remote stores land in the owner's HBM, the system-scope fence after them
+// orders data before flag, and the data is read back with system-scope loads.
+__device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc& x, int row, uint32_t* fault, f32x4 g, int64_t i0,
+                                           bool act, int b, uint32_t ep) {
+  const int W = x.world, r = x.rank, lane = threadIdx.x & 63;
+  const int slot = (int)(ep & 1u);
+  const int64_t my_row = ((int64_t)slot * W + r) * x.pt + i0;
+  for (int q = 0; q < W; ++q)
+    if (q != r && act) *reinterpret_cast<f32x4*>(x.data[q] + my_row) = g;
+  __threadfence_system();
+  const int64_t fl_from_me = ((int64_t)r * MDP_XCH_NETS + row) * MDP_XCH_FCH + b;
+  if (lane < W && lane != r)
+    __hip_atomic_store(x.flags[lane] + fl_from_me, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const bool gone = __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (lane < W && lane != r && !gone) {
+    const uint32_t* fl = x.flags[r] + ((int64_t)lane * MDP_XCH_NETS + row) * MDP_XCH_FCH + b;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(__hip_atomic_load(const_cast<uint32_t*>(fl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
+        __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __threadfence_system();
+  if (!act) return g;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < W; ++q) {
+    const f32x4 v = q == r ? g : ld_sys4(x.data[r] + ((int64_t)slot * W + q) * x.pt + i0);
+    s = q == 0 ? v : s + v;
+  }
+  return s;
+}
 }  // namespace
+
+// connection probe: chunk b carries value (q + 1) * 4096 + ((param + 7 ep) %
+// 4096) from rank q (exact in fp32), so the world sum is known in closed form
+// and differs between the epochs that reuse a slot
+__global__ __launch_bounds__(64) void k_xchg_probe(const XchgDesc* xd, uint32_t ep, uint32_t* bad, uint32_t* fault) {
+  const XchgDesc& x = *xd;
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int64_t i0 = (int64_t)b * MDP_RA_CHUNK + 4 * lane;
+  f32x4 g, want;
+  for (int j = 0; j < 4; ++j) {
+    const float base = (float)((i0 + j + 7 * (int64_t)ep) % 4096);
+    g[j] = (float)((x.rank + 1) * 4096) + base;
+    float w = 0.f;
+    for (int q = 0; q < x.world; ++q) w += (float)((q + 1) * 4096) + base;
+    want[j] = w;
+  }
+  const f32x4 s = xchg_chunk(x, MDP_XCH_PROBE_ROW, fault, g, i0, true, b, ep);
+  uint32_t nbad = 0;
+  for (int j = 0; j < 4; ++j) nbad += s[j] != want[j] ? 1u : 0u;
+  if (nbad) atomicAdd(bad, nbad);
+}
+
+hipError_t mdp_launch_xchg_probe(const XchgDesc* xd, uint32_t ep, int nchunk, uint32_t* bad, uint32_t* fault,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(k_xchg_probe, dim3(nchunk), dim3(64), 0, s, xd, ep, bad, fault);
+  return hipGetLastError();
+}
 
 // b: this workgroup's index among the nb workgroups of this net's step
 __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const int b, const uint32_t nb) {
@@ -53,6 +137,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     // Adam state of the chunk, requested with the partial-gradient loads
     f32x4 m4 = {0.f, 0.f, 0.f, 0.f}, v4 = m4, th4 = m4, tg4 = m4;
     const float b1p = a.beta[0], b2p = a.beta[1];  // this step's powers (advanced at the end)
+    const uint32_t ep = f.phase == 3 ? f.xstep[0] + 1u : 0u;  // exchange epoch (advanced at the end)
     if (grp == 0 && act) {
       m4 = ld4(a.m + i0);
       v4 = ld4(a.v + i0);
@@ -79,6 +164,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       f32x4 g = red[0][col];
 #pragma unroll
       for (int q = 1; q < 16; ++q) g += red[q][col];
+      if (f.phase == 3) g = xchg_chunk(*f.xd, f.net_id, &a.ctl->fault, g, i0, act, b, ep);
       double ss = 0.0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -197,6 +283,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       a.beta[0] = p1 * a.b1;
       a.beta[1] = p2 * a.b2;
       if (a.bump_ctr) a.ctl->upd_ctr += (uint32_t)a.bump_ctr;
+      if (f.phase == 3) f.xstep[0] += 1u;
     }
   }
 }

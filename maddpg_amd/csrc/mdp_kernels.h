@@ -93,13 +93,43 @@ struct ApplyArgs {
 // k_reduce_apply (mdp_apply_fused.hip): batch reduction + optimizer step in one launch
 #define MDP_RA_CHUNK 256   // parameters per workgroup
 #define MDP_RA_MAXCH 256   // chunks per tensor the sync area holds
+// Direct xGMI gradient exchange of the data-parallel step (phase 3 below):
+// every rank owns one exchange buffer (uncached device memory, IPC-exported)
+// laid out as
+//   data  [2 slots][world][PT] fp32   -- slot = exchange epoch & 1
+//   flags [world][MDP_XCH_NETS][MDP_XCH_FCH] uint32 -- last epoch received
+// and holds every peer's buffer mapped (hipIpcOpenMemHandle).  Rank r pushes
+// its reduced chunk into data[slot][r] of every peer, then (release, system
+// scope) stores the epoch into the peer's flags[r][net][chunk]; the receiver
+// waits for all flags of its chunk and sums the world contributions in rank
+// order -- every rank computes the identical sum, so replicas stay bit-equal.
+// Flag row 2 * MDP_MAX_AGENTS belongs to the connection probe (k_xchg_probe).
+#define MDP_XCH_FCH 1024     // chunk flags per net
+#define MDP_XCH_MAXW 8
+#define MDP_XCH_NETS (2 * MDP_MAX_AGENTS + 1)
+#define MDP_XCH_PROBE_ROW (2 * MDP_MAX_AGENTS)
+struct XchgDesc {
+  int world, rank;
+  int64_t pt;                        // floats per slot row (param-space length)
+  float* data[MDP_XCH_MAXW];         // rank q's exchange buffer in this process (data[rank] local)
+  uint32_t* flags[MDP_XCH_MAXW];
+};
+inline int64_t mdp_xch_data_bytes(int world, int64_t pt) { return 4 * (2 * (int64_t)world * pt); }
+inline int64_t mdp_xch_bytes(int world, int64_t pt) {
+  return mdp_xch_data_bytes(world, pt) + 4 * (int64_t)world * MDP_XCH_NETS * MDP_XCH_FCH;
+}
+
 struct FusedApplyArgs {
   ApplyArgs ap;         // ap.slab / nwg / slab_stride: the partial gradients
   int rblk[7];          // prefix counts of MDP_RA_CHUNK workgroups per tensor of ap.net
   uint32_t* sync_ctr;   // 6 tensor counters of this (agent, net), 32 words apart
   double* sync_part;    // [6][MDP_RA_MAXCH] published sums of squares
   uint32_t* done_ctr;   // workgroups finished (last one advances beta)
-  int phase;            // 0 reduce + step; 1 reduce into grad[] only; 2 step from grad[] (all-reduced)
+  int phase;            // 0 reduce + step; 1 reduce into grad[] only; 2 step from grad[] (all-reduced);
+                        // 3 reduce, xGMI exchange with every rank (xd), step x ap.scale
+  const XchgDesc* xd;   // phase 3: device copy of the exchange descriptor
+  int net_id;           // phase 3: 2 * agent + net (flag row and epoch counter)
+  uint32_t* xstep;      // phase 3: Ctl::xstep[net_id], exchanges done for this net
 };
 // sync area: per (agent, net) 8 counters x 128 B, then [6][MAXCH] doubles
 inline int64_t mdp_ra_sync_bytes() {
@@ -227,6 +257,11 @@ struct RaBatch {
 };
 int mdp_ra_grid(const FusedApplyArgs& f);
 hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s);
+// connection probe of the xGMI exchange: nchunk chunks of a rank-tagged
+// pattern through the same exchange code, *bad += mismatching parameters,
+// *fault = 2 when a peer's flag did not arrive in time
+hipError_t mdp_launch_xchg_probe(const XchgDesc* xd, uint32_t ep, int nchunk, uint32_t* bad, uint32_t* fault,
+                                 hipStream_t s);
 hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t s);
 hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
                              hipStream_t s);

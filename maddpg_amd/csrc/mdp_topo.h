@@ -58,5 +58,6 @@ struct Ctl {
   int64_t episodes;     // finished episodes logged
   uint32_t ticket[8];   // last-workgroup tickets
   uint32_t upd_ctr;     // RNG counter for training noise
-  uint32_t fault;       // set by a bounded spin that timed out (k_reduce_apply)
+  uint32_t fault;       // set by a bounded spin that timed out (1 norm handshake, 2 xGMI exchange)
+  uint32_t xstep[16];   // xGMI exchanges completed per net (2 * agent + net): the epoch counter
 };

@@ -389,6 +389,63 @@ class Engine:
         self.dp_init(world, rank, obj[0])
         return True
 
+    def dp_xgmi_open(self, world, rank):
+        """export this rank's exchange buffer; returns its 64-byte IPC handle"""
+        buf = ctypes.create_string_buffer(64)
+        self._c("mdp_dp_xgmi_open", int(world), int(rank), buf)
+        return buf.raw
+
+    def dp_xgmi_connect(self, handles):
+        self._c("mdp_dp_xgmi_connect", b"".join(bytes(x) for x in handles))
+
+    def dp_xgmi_probe(self):
+        bad = ctypes.c_int32(0)
+        self._c("mdp_dp_xgmi_probe", ctypes.byref(bad))
+        return bad.value
+
+    def dp_xgmi_init_from_dist(self, world, rank):
+        """Direct xGMI gradient exchange (mdp_dp_xgmi_*): all-gather the IPC
+        handles over torch.distributed, map every peer, run the probe, and
+        enable only when every rank succeeded at every stage.  Returns False
+        (everything torn down on every rank) otherwise, so the caller can fall
+        back to dp_init_from_dist."""
+        import torch.distributed as dist
+
+        def agree(ok):
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                             device=self.device if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t.item())
+
+        err = None
+        try:
+            handle = self.dp_xgmi_open(world, rank)
+        except Exception as e:  # noqa: BLE001 -- reported, then every rank falls back together
+            handle, err = None, e
+        handles = [None] * world
+        dist.all_gather_object(handles, handle)
+        ok = all(x is not None for x in handles)
+        if ok:
+            try:
+                self.dp_xgmi_connect(handles)
+            except Exception as e:  # noqa: BLE001
+                ok, err = False, e
+        ok = agree(ok)
+        if ok:
+            try:
+                self.dp_xgmi_probe()
+            except Exception as e:  # noqa: BLE001
+                ok, err = False, e
+            ok = agree(ok)
+        if ok:
+            self._c("mdp_dp_xgmi_enable")
+        else:
+            self._c("mdp_dp_xgmi_close")
+            if err is not None:
+                import sys
+                print(f"[rank {rank}] xGMI exchange unavailable ({err}); using RCCL", file=sys.stderr)
+        return ok
+
     def set_graphs(self, on=True):
         """hipGraph replay of update_round (default on; per-kernel profiling runs eager)."""
         self._c("mdp_set_graphs", 1 if on else 0)

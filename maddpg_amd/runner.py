@@ -51,10 +51,19 @@ class VecRunner:
         self._allreduce = make_allreduce(self.eng.stream) if world_size > 1 else None
         # native data parallelism: the library's own RCCL communicator, so a whole
         # vector step (rollout + due rounds with their all-reduces) is one C call;
-        # MDP_NATIVE_DP=0 keeps the torch.distributed path (strict_round)
+        # MDP_NATIVE_DP=0 keeps the torch.distributed path (strict_round).  The
+        # exchange is the direct xGMI one inside the optimizer kernel when every
+        # rank can map every peer (MDP_DP_XGMI=0: RCCL all-reduces instead)
         self.native_dp = False
+        self.dp_kind = None
         if world_size > 1 and os.environ.get("MDP_NATIVE_DP", "1") == "1":
-            self.native_dp = self.eng.dp_init_from_dist(world_size, rank)
+            if os.environ.get("MDP_DP_XGMI", "1") == "1" and self.eng.dp_xgmi_init_from_dist(world_size, rank):
+                self.native_dp, self.dp_kind = True, "native-xgmi"
+            else:
+                self.native_dp = self.eng.dp_init_from_dist(world_size, rank)
+                self.dp_kind = "native-rccl" if self.native_dp else None
+        if world_size > 1 and self.dp_kind is None:
+            self.dp_kind = "torch.distributed"
 
     def rollout(self):
         self.eng.env_step()
