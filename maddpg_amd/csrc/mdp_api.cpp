@@ -1394,6 +1394,7 @@ int mdp_dp_xgmi_enable(mdp_handle* h) {
 
 int mdp_dp_xgmi_close(mdp_handle* h) {
   if (!h) return -1;
+  (void)hipGetLastError();  // a failed open/map must not surface at the next launch check
   if (h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
   xgmi_release(h);
   if (!h->comm) h->dp_world = 1;
