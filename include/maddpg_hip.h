@@ -188,7 +188,7 @@ int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank
  * throughput).  Handshake (every rank, in order):
  *   open(world, rank) -> its 64-byte IPC handle; the caller all-gathers the
  *   handles; connect(handles[world][64]); probe() exchanges a known pattern
- *   (0 = every value arrived; fails after 10 s without a peer); the caller
+ *   (0 = every value arrived; fails after 30 s without a peer); the caller
  *   agrees on success across ranks, then enable() -- or close() everywhere and
  *   fall back to mdp_dp_init.  world 2..8. */
 #define MDP_XGMI_HANDLE_BYTES 64

@@ -972,7 +972,7 @@ int mdp_synchronize(mdp_handle* h) {
   uint32_t fault = 0;
   HIPCHK(h, hipMemcpy(&fault, &h->ctl->fault, sizeof(fault), hipMemcpyDeviceToHost));
   if (fault == 1) return fail(h, "device fault: a tensor-norm handshake timed out (k_reduce_apply)");
-  if (fault == 2) return fail(h, "device fault: a data-parallel peer did not reach the xGMI exchange within 10 s");
+  if (fault == 2) return fail(h, "device fault: a data-parallel peer did not reach the xGMI exchange within 30 s");
   if (fault) return fail(h, "device fault");
   return 0;
 }
@@ -1377,7 +1377,7 @@ int mdp_dp_xgmi_probe(mdp_handle* h, int32_t* mismatches) {
   HIPCHK(h, hipMemcpyAsync(res, h->x_probe, sizeof(res), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (mismatches) *mismatches = (int32_t)res[0];
-  if (res[1]) return fail(h, "mdp_dp_xgmi_probe: a peer did not reach the exchange within 10 s");
+  if (res[1]) return fail(h, "mdp_dp_xgmi_probe: a peer did not reach the exchange within 30 s");
   if (res[0]) return fail(h, "mdp_dp_xgmi_probe: exchanged values differ from the expected world sum");
   return 0;
 }

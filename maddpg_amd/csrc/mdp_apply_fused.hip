@@ -34,10 +34,10 @@ __device__ __forceinline__ double ld_agent(const double* p) {
   return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// a peer that has not arrived after this long (s_memrealtime runs at 100 MHz)
+// a peer that has not arrived after 30 s (s_memrealtime runs at 100 MHz)
 // is taken to be gone: the wait records Ctl::fault = 2 and gives up, and later
 // exchanges skip their waits (the host reports the fault at the next sync)
-constexpr uint64_t kXchgTimeoutTicks = 10ull * 100000000ull;
+constexpr uint64_t kXchgTimeoutTicks = 30ull * 100000000ull;
 
 // system-scope (cache-bypassing) load of 4 floats a peer wrote into our buffer
 __device__ __forceinline__ f32x4 ld_sys4(const float* p) {
