@@ -294,7 +294,7 @@ struct mdp_handle {
   RaBatch tp_xchg;                    // data parallel over xGMI: reduce + exchange + step (x 1/G)
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
-  float* xbuf = nullptr;
+  uint64_t* xbuf = nullptr;
   int x_world = 0, x_rank = 0;
   std::vector<void*> x_opened;        // peer buffers opened with hipIpcOpenMemHandle
   XchgDesc* xd_dev = nullptr;
@@ -1319,13 +1319,12 @@ int mdp_dp_xgmi_open(mdp_handle* h, int32_t world, int32_t rank, uint8_t* handle
   for (int i = 0; i < h->cfg.n_agents; ++i)
     for (int net = 0; net < 2; ++net) {
       if (!reduce_apply_ok(h, i, net)) return fail(h, "the xGMI exchange needs the fused optimizer kernel");
-      if (fused_args_for(h, i, net).rblk[6] > MDP_XCH_FCH) return fail(h, "net too large for the exchange flags");
     }
   HIPCHK(h, hipSetDevice(h->device));
   const int64_t bytes = mdp_xch_bytes(world, h->L.PT);
   void* p = nullptr;
   HIPCHK(h, hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached));
-  h->xbuf = (float*)p;
+  h->xbuf = (uint64_t*)p;
   HIPCHK(h, hipMemset(p, 0, (size_t)bytes));
   HIPCHK(h, hipMalloc((void**)&h->x_probe, 2 * sizeof(uint32_t)));
   HIPCHK(h, hipDeviceSynchronize());
@@ -1347,7 +1346,7 @@ int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles) {
   std::memset(&xd, 0, sizeof(xd));
   xd.world = W;
   xd.rank = r;
-  xd.pt = h->L.PT;
+  xd.pt = h->L.PT + MDP_XCH_PROBE;
   h->x_opened.assign(W, nullptr);
   for (int q = 0; q < W; ++q) {
     void* base = h->xbuf;
@@ -1358,8 +1357,7 @@ int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles) {
       if (e != hipSuccess) return fail(h, "hipIpcOpenMemHandle", e);
       h->x_opened[q] = base;
     }
-    xd.data[q] = (float*)base;
-    xd.flags[q] = (uint32_t*)((char*)base + mdp_xch_data_bytes(W, h->L.PT));
+    xd.data[q] = (uint64_t*)base;
   }
   HIPCHK(h, hipMalloc((void**)&h->xd_dev, sizeof(XchgDesc)));
   HIPCHK(h, hipMemcpy(h->xd_dev, &xd, sizeof(XchgDesc), hipMemcpyHostToDevice));
@@ -1368,8 +1366,7 @@ int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles) {
 
 int mdp_dp_xgmi_probe(mdp_handle* h, int32_t* mismatches) {
   if (!h || !h->xd_dev) return fail(h, "mdp_dp_xgmi_probe: not connected");
-  const int nchunk = (int)std::min<int64_t>(8, h->L.PT / MDP_RA_CHUNK);
-  if (nchunk < 1) return fail(h, "mdp_dp_xgmi_probe: parameter space too small");
+  const int nchunk = MDP_XCH_PROBE / 256;
   HIPCHK(h, hipMemsetAsync(h->x_probe, 0, 2 * sizeof(uint32_t), h->stream));
   for (int k = 0; k < 4; ++k)  // both slots, each reused once
     HIPCHK(h, mdp_launch_xchg_probe(h->xd_dev, ++h->x_probe_ep, nchunk, h->x_probe, h->x_probe + 1, h->stream));

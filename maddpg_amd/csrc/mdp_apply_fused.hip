@@ -3,7 +3,7 @@
 // into grad[]) -> ncclAllReduce -> phase 2 (step).  Data parallel over the
 // direct xGMI exchange: phase 3, still ONE launch -- each chunk workgroup
 // pushes its reduced chunk to every peer and sums the world's chunks in rank
-// order before the clip/Adam below (xchg_chunk).
+// order before the clip/Adam below (xchg_chunk, LL protocol).
 //
 // Workgroup (tensor t, chunk c) of 256 parameters, 1024 threads: 16 groups of
 // 64 threads each sum a quarter-ish of the per-workgroup partial gradients of
@@ -39,73 +39,72 @@ __device__ __forceinline__ double ld_agent(const double* p) {
 // exchanges skip their waits (the host reports the fault at the next sync)
 constexpr uint64_t kXchgTimeoutTicks = 30ull * 100000000ull;
 
-// system-scope (cache-bypassing) load of 4 floats a peer wrote into our buffer
-__device__ __forceinline__ f32x4 ld_sys4(const float* p) {
-  uint32_t* u = reinterpret_cast<uint32_t*>(const_cast<float*>(p));
-  f32x4 v;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    v[j] = __uint_as_float(__hip_atomic_load(u + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  return v;
+__device__ __forceinline__ uint64_t ll_word(float v, uint32_t ep) {
+  return ((uint64_t)ep << 32) | (uint64_t)__float_as_uint(v);
 }
 
-// The xGMI exchange of one 256-parameter chunk (flag row `row`, chunk b),
-// run by ONE wave.  g: this rank's reduced chunk (lane = 4 parameters at
-// param-space offset i0); returns the sum over ranks in rank order (identical
-// on every rank).  The exchange buffers are uncached device memory: the
-// remote stores land in the owner's HBM, the system-scope fence after them
-// orders data before flag, and the data is read back with system-scope loads.
-__device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc& x, int row, uint32_t* fault, f32x4 g, int64_t i0,
-                                           bool act, int b, uint32_t ep) {
-  const int W = x.world, r = x.rank, lane = threadIdx.x & 63;
-  const int slot = (int)(ep & 1u);
-  const int64_t my_row = ((int64_t)slot * W + r) * x.pt + i0;
-  for (int q = 0; q < W; ++q)
-    if (q != r && act) *reinterpret_cast<f32x4*>(x.data[q] + my_row) = g;
-  __threadfence_system();
-  const int64_t fl_from_me = ((int64_t)r * MDP_XCH_NETS + row) * MDP_XCH_FCH + b;
-  if (lane < W && lane != r)
-    __hip_atomic_store(x.flags[lane] + fl_from_me, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const bool gone = __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-  if (lane < W && lane != r && !gone) {
-    const uint32_t* fl = x.flags[r] + ((int64_t)lane * MDP_XCH_NETS + row) * MDP_XCH_FCH + b;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(__hip_atomic_load(const_cast<uint32_t*>(fl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
-        __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+// The xGMI exchange of 4 parameters per lane at param-space offset i0 (LL
+// protocol, see XchgDesc), run by ONE wave.  g: this rank's reduced values;
+// returns the sum over ranks in rank order (identical on every rank).  A
+// bounded wait (30 s on the 100 MHz real-time clock) records *fault = 2 and
+// gives up; once a fault is recorded later exchanges do not wait.
+__device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc& x, uint32_t* fault, f32x4 g, int64_t i0, bool act,
+                                           uint32_t ep) {
+  const int W = x.world, r = x.rank;
+  const int64_t slot_row = (int64_t)(ep & 1u) * W;
+  if (act) {
+    uint64_t* mine = nullptr;
+    for (int q = 0; q < W; ++q) {
+      if (q == r) continue;
+      mine = x.data[q] + (slot_row + r) * x.pt + i0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __hip_atomic_store(mine + j, ll_word(g[j], ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  __threadfence_system();
-  if (!act) return g;
+  const bool gone = __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  uint64_t t0 = 0;
   for (int q = 0; q < W; ++q) {
-    const f32x4 v = q == r ? g : ld_sys4(x.data[r] + ((int64_t)slot * W + q) * x.pt + i0);
+    f32x4 v = g;
+    if (q != r && act) {
+      uint64_t* src = x.data[r] + (slot_row + q) * x.pt + i0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint64_t w = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        while ((uint32_t)(w >> 32) != ep && !gone) {
+          __builtin_amdgcn_s_sleep(1);
+          if (t0 == 0) t0 = __builtin_amdgcn_s_memrealtime();
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
+            __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          w = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        v[j] = __uint_as_float((uint32_t)w);
+      }
+    }
     s = q == 0 ? v : s + v;
   }
-  return s;
+  return act ? s : g;
 }
 }  // namespace
 
-// connection probe: chunk b carries value (q + 1) * 4096 + ((param + 7 ep) %
-// 4096) from rank q (exact in fp32), so the world sum is known in closed form
-// and differs between the epochs that reuse a slot
+// connection probe: word i of the probe area carries (q + 1) * 4096 +
+// ((i + 7 ep) % 4096) from rank q (exact in fp32), so the world sum is known
+// in closed form and differs between the epochs that reuse a slot
 __global__ __launch_bounds__(64) void k_xchg_probe(const XchgDesc* xd, uint32_t ep, uint32_t* bad, uint32_t* fault) {
   const XchgDesc& x = *xd;
-  const int b = blockIdx.x, lane = threadIdx.x;
-  const int64_t i0 = (int64_t)b * MDP_RA_CHUNK + 4 * lane;
+  const int64_t p0 = (int64_t)blockIdx.x * 256 + 4 * threadIdx.x;  // within the probe area
   f32x4 g, want;
   for (int j = 0; j < 4; ++j) {
-    const float base = (float)((i0 + j + 7 * (int64_t)ep) % 4096);
+    const float base = (float)((p0 + j + 7 * (int64_t)ep) % 4096);
     g[j] = (float)((x.rank + 1) * 4096) + base;
     float w = 0.f;
     for (int q = 0; q < x.world; ++q) w += (float)((q + 1) * 4096) + base;
     want[j] = w;
   }
-  const f32x4 s = xchg_chunk(x, MDP_XCH_PROBE_ROW, fault, g, i0, true, b, ep);
+  const f32x4 s = xchg_chunk(x, fault, g, x.pt - MDP_XCH_PROBE + p0, true, ep);
   uint32_t nbad = 0;
   for (int j = 0; j < 4; ++j) nbad += s[j] != want[j] ? 1u : 0u;
   if (nbad) atomicAdd(bad, nbad);
@@ -164,7 +163,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       f32x4 g = red[0][col];
 #pragma unroll
       for (int q = 1; q < 16; ++q) g += red[q][col];
-      if (f.phase == 3) g = xchg_chunk(*f.xd, f.net_id, &a.ctl->fault, g, i0, act, b, ep);
+      if (f.phase == 3) g = xchg_chunk(*f.xd, &a.ctl->fault, g, i0, act, ep);
       double ss = 0.0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {

@@ -95,28 +95,26 @@ struct ApplyArgs {
 #define MDP_RA_MAXCH 256   // chunks per tensor the sync area holds
 // Direct xGMI gradient exchange of the data-parallel step (phase 3 below):
 // every rank owns one exchange buffer (uncached device memory, IPC-exported)
-// laid out as
-//   data  [2 slots][world][PT] fp32   -- slot = exchange epoch & 1
-//   flags [world][MDP_XCH_NETS][MDP_XCH_FCH] uint32 -- last epoch received
-// and holds every peer's buffer mapped (hipIpcOpenMemHandle).  Rank r pushes
-// its reduced chunk into data[slot][r] of every peer, then (release, system
-// scope) stores the epoch into the peer's flags[r][net][chunk]; the receiver
-// waits for all flags of its chunk and sums the world contributions in rank
-// order -- every rank computes the identical sum, so replicas stay bit-equal.
-// Flag row 2 * MDP_MAX_AGENTS belongs to the connection probe (k_xchg_probe).
-#define MDP_XCH_FCH 1024     // chunk flags per net
+// of 64-bit words laid out as
+//   [2 slots][world][PT + MDP_XCH_PROBE]   word = epoch << 32 | fp32 bits
+// (slot = exchange epoch & 1; the last MDP_XCH_PROBE words of a row belong
+// to the connection probe) and holds every peer's buffer mapped
+// (hipIpcOpenMemHandle).  Rank r stores each value of its reduced chunk, tagged
+// with the epoch, into row [slot][r] of every peer with ONE 64-bit
+// system-scope store; the receiver polls each word of its peers' rows until
+// the tag equals the epoch (data and flag arrive together: no fences, no
+// separate flag round trip -- the LL protocol) and sums the world's values in
+// rank order, so every rank computes the identical sum and replicas stay
+// bit-equal.  Epoch 0 never occurs (the buffer starts zeroed).
 #define MDP_XCH_MAXW 8
-#define MDP_XCH_NETS (2 * MDP_MAX_AGENTS + 1)
-#define MDP_XCH_PROBE_ROW (2 * MDP_MAX_AGENTS)
+#define MDP_XCH_PROBE 2048   // probe words per row (8 chunks)
 struct XchgDesc {
   int world, rank;
-  int64_t pt;                        // floats per slot row (param-space length)
-  float* data[MDP_XCH_MAXW];         // rank q's exchange buffer in this process (data[rank] local)
-  uint32_t* flags[MDP_XCH_MAXW];
+  int64_t pt;                        // words per row: param-space length + MDP_XCH_PROBE
+  uint64_t* data[MDP_XCH_MAXW];      // rank q's exchange buffer in this process (data[rank] local)
 };
-inline int64_t mdp_xch_data_bytes(int world, int64_t pt) { return 4 * (2 * (int64_t)world * pt); }
-inline int64_t mdp_xch_bytes(int world, int64_t pt) {
-  return mdp_xch_data_bytes(world, pt) + 4 * (int64_t)world * MDP_XCH_NETS * MDP_XCH_FCH;
+inline int64_t mdp_xch_bytes(int world, int64_t param_floats) {
+  return 8 * (2 * (int64_t)world * (param_floats + MDP_XCH_PROBE));
 }
 
 struct FusedApplyArgs {
@@ -128,7 +126,7 @@ struct FusedApplyArgs {
   int phase;            // 0 reduce + step; 1 reduce into grad[] only; 2 step from grad[] (all-reduced);
                         // 3 reduce, xGMI exchange with every rank (xd), step x ap.scale
   const XchgDesc* xd;   // phase 3: device copy of the exchange descriptor
-  int net_id;           // phase 3: 2 * agent + net (flag row and epoch counter)
+  int net_id;           // phase 3: 2 * agent + net (epoch counter)
   uint32_t* xstep;      // phase 3: Ctl::xstep[net_id], exchanges done for this net
 };
 // sync area: per (agent, net) 8 counters x 128 B, then [6][MAXCH] doubles
