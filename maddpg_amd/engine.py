@@ -404,46 +404,31 @@ class Engine:
         return bad.value
 
     def dp_xgmi_init_from_dist(self, world, rank):
-        """Direct xGMI gradient exchange (mdp_dp_xgmi_*): all-gather the IPC
-        handles over torch.distributed, map every peer, run the probe, and
-        enable only when every rank succeeded at every stage.  Returns False
-        (everything torn down on every rank) otherwise, so the caller can fall
-        back to dp_init_from_dist."""
-        import torch.distributed as dist
+        """Direct xGMI gradient exchange (mdp_dp_xgmi_*): the handshake of
+        parallel.xgmi_handshake over torch.distributed.  Returns False
+        (everything torn down on every rank) when any rank failed, so the
+        caller can fall back to dp_init_from_dist."""
+        from .parallel import xgmi_handshake
+        eng = self
 
-        def agree(ok):
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                             device=self.device if dist.get_backend() == "nccl" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            return bool(t.item())
+        class _Ops:
+            device = eng.device
+            open = staticmethod(eng.dp_xgmi_open)
+            connect = staticmethod(eng.dp_xgmi_connect)
+            probe = staticmethod(eng.dp_xgmi_probe)
 
-        err = None
-        try:
-            handle = self.dp_xgmi_open(world, rank)
-        except Exception as e:  # noqa: BLE001 -- reported, then every rank falls back together
-            handle, err = None, e
-        handles = [None] * world
-        dist.all_gather_object(handles, handle)
-        ok = all(x is not None for x in handles)
-        if ok:
-            try:
-                self.dp_xgmi_connect(handles)
-            except Exception as e:  # noqa: BLE001
-                ok, err = False, e
-        ok = agree(ok)
-        if ok:
-            try:
-                self.dp_xgmi_probe()
-            except Exception as e:  # noqa: BLE001
-                ok, err = False, e
-            ok = agree(ok)
-        if ok:
-            self._c("mdp_dp_xgmi_enable")
-        else:
-            self._c("mdp_dp_xgmi_close")
-            if err is not None:
-                import sys
-                print(f"[rank {rank}] xGMI exchange unavailable ({err}); using RCCL", file=sys.stderr)
+            @staticmethod
+            def enable():
+                eng._c("mdp_dp_xgmi_enable")
+
+            @staticmethod
+            def close():
+                eng._c("mdp_dp_xgmi_close")
+
+        ok, err = xgmi_handshake(_Ops, world, rank)
+        if not ok and err is not None:
+            import sys
+            print(f"[rank {rank}] xGMI exchange unavailable ({err}); using RCCL", file=sys.stderr)
         return ok
 
     def set_graphs(self, on=True):

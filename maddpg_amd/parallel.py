@@ -100,3 +100,45 @@ class EngineOps:
 
     def apply_grad(self, i, net, scale):
         self.eng.apply_grad(i, net, scale)
+
+
+def xgmi_handshake(ops, world, rank):
+    """Set-up of the direct xGMI gradient exchange (mdp_dp_xgmi_*), every rank
+    in step over torch.distributed.  ops: open(world, rank) -> 64-byte handle,
+    connect(handles in rank order), probe(), enable(), close() -- the Engine on
+    a GPU, a stand-in in the CPU (gloo) tests.  Enables only when every rank
+    succeeded at every stage; otherwise closes it on every rank and returns
+    (False, error of this rank or None) so all ranks fall back together."""
+    dev = getattr(ops, "device", None)
+
+    def agree(ok):
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    err = None
+    try:
+        handle = ops.open(world, rank)
+    except Exception as e:  # noqa: BLE001 -- every rank falls back together
+        handle, err = None, e
+    handles = [None] * world
+    dist.all_gather_object(handles, handle)
+    ok = all(x is not None for x in handles)
+    if ok:
+        try:
+            ops.connect(handles)
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, e
+    ok = agree(ok)
+    if ok:
+        try:
+            ops.probe()
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, e
+        ok = agree(ok)
+    if ok:
+        ops.enable()
+    else:
+        ops.close()
+    return ok, err

@@ -1,0 +1,94 @@
+"""Host logic of the direct xGMI exchange set-up (parallel.xgmi_handshake) on
+CPU: world_size 2 over gloo with stand-in ops.  Every rank must end in the
+same state -- all enabled, or all closed (so they fall back to RCCL
+together) -- whichever rank fails at whichever stage."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from maddpg_amd.parallel import xgmi_handshake
+
+
+class FakeOps:
+    def __init__(self, rank, fail_at):
+        self.rank, self.fail_at, self.log = rank, fail_at, []
+
+    def _step(self, name):
+        self.log.append(name)
+        if self.fail_at == name:
+            raise RuntimeError(f"{name} failed on rank {self.rank}")
+
+    def open(self, world, rank):
+        self._step("open")
+        return bytes([rank]) * 64
+
+    def connect(self, handles):
+        self._step("connect")
+        self.handles = handles
+
+    def probe(self):
+        self._step("probe")
+
+    def enable(self):
+        self.log.append("enable")
+
+    def close(self):
+        self.log.append("close")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fail_rank, fail_at, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ops = FakeOps(rank, fail_at if rank == fail_rank else None)
+    ok, err = xgmi_handshake(ops, world, rank)
+    q.put((rank, ok, err is not None, ops.log, getattr(ops, "handles", None)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(fail_rank, fail_at, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fail_rank, fail_at, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict((item[0], item[1:]) for item in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_all_ranks_enable_with_handles_in_rank_order():
+    got = _run(None, None)
+    for r in range(2):
+        ok, has_err, log, handles = got[r]
+        assert ok and not has_err
+        assert log == ["open", "connect", "probe", "enable"]
+        assert handles == [bytes([0]) * 64, bytes([1]) * 64]
+
+
+@pytest.mark.parametrize("fail_rank,fail_at", [(1, "open"), (0, "connect"), (1, "probe")])
+def test_any_failure_closes_every_rank(fail_rank, fail_at):
+    got = _run(fail_rank, fail_at)
+    for r in range(2):
+        ok, has_err, log, _ = got[r]
+        assert not ok
+        assert log[-1] == "close" and "enable" not in log
+        assert has_err == (r == fail_rank)
+        if fail_at == "open":   # nobody connects when a handle is missing
+            assert "connect" not in log
+        if fail_at == "probe":  # every rank ran the probe (its peers wait on it)
+            assert "probe" in log
