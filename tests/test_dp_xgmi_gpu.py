@@ -1,7 +1,7 @@
 """Direct xGMI gradient exchange (mdp_dp_xgmi_*: the exchange inside the fused
 optimizer kernel).
 
-Runs two rank processes on ONE visible GPU (the IPC mapping, the flag protocol
+Runs two rank processes on ONE visible GPU (the IPC mapping, the LL protocol
 and the rank-order sum are the same code as across GPUs; only the link
 differs), with a gloo process group for the handle exchange:
 
@@ -11,7 +11,8 @@ differs), with a gloo process group for the handle exchange:
   equal an undistributed single-GPU run bit for bit -- strict and throughput
   mode, eager and graph-replayed;
 * ranks with their own env copies and index streams (the real sharding): the
-  replicas stay bit-identical and finite.
+  replicas stay bit-identical and finite;
+* four ranks (three peers per exchange).
 """
 import os
 import socket
@@ -96,12 +97,12 @@ def _rank_main(rank, world, port, q, mode, identical, graphs):
         raise
 
 
-def _run(mode, identical, graphs=True):
+def _run(mode, identical, graphs=True, world=2):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, q, mode, identical, graphs)) for r in range(2)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q, mode, identical, graphs)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
@@ -132,3 +133,13 @@ def test_xgmi_sharded_replicas_identical(mode):
     assert np.all(np.isfinite(got[0][2]))
     # the shards really differ: each rank's own batch statistics
     assert not np.array_equal(got[0][3], got[1][3])
+
+
+def test_xgmi_four_ranks():
+    """world 4 (rank-order sum over 3 peers), identical data: the four replicas
+    are bit-identical, and match the single-GPU run up to the rounding of the
+    partial sum 3g (((g + g) + g) + g) / 4 need not be exactly g)."""
+    got = _run("strict", True, True, world=4)
+    for r in range(1, 4):
+        np.testing.assert_array_equal(got[r][2], got[0][2])
+    np.testing.assert_allclose(got[0][2], got[0][4], rtol=1e-5, atol=1e-6)
