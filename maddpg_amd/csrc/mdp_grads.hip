@@ -25,6 +25,10 @@
 #include "mdp_device.h"
 #include "mdp_kernels.h"
 
+#ifndef MDP_GEN_THREADS
+#define MDP_GEN_THREADS 1024  // 16 waves: 4 per SIMD to cover the weight-chunk latency
+#endif
+
 namespace {
 // Y[16][col tile nt] = act(X[16][K] @ W[K][N] + b), weights in 64-deep chunks, the next in flight
 template <bool RELU>
@@ -156,7 +160,7 @@ __device__ __forceinline__ void wgrad_tile(const float* X, int ldx, int K, const
 }  // namespace
 
 template <int H>
-__global__ __launch_bounds__(512) void k_critic_grad(CriticArgs a) {
+__global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   constexpr int NT = H / 16;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Topo& T = a.topo;
@@ -343,7 +347,7 @@ __global__ __launch_bounds__(512) void k_critic_grad(CriticArgs a) {
 }
 
 template <int H>
-__global__ __launch_bounds__(512) void k_actor_grad(ActorArgs a) {
+__global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   constexpr int NT = H / 16;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Topo& T = a.topo;
@@ -507,7 +511,7 @@ hipError_t launch_critic(const CriticArgs& a, int lds, hipStream_t s) {
     (void)hipGetLastError();
     attr = true;
   }
-  hipLaunchKernelGGL(k_critic_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(k_critic_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(MDP_GEN_THREADS), lds, s, a);
   return hipGetLastError();
 }
 template <int H>
@@ -519,7 +523,7 @@ hipError_t launch_actor(const ActorArgs& a, int lds, hipStream_t s) {
     (void)hipGetLastError();
     attr = true;
   }
-  hipLaunchKernelGGL(k_actor_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(512), lds, s, a);
+  hipLaunchKernelGGL(k_actor_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(MDP_GEN_THREADS), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace
