@@ -3,13 +3,15 @@
 // configs[4]: simple_tag N=6, H=128, B=4096).  The register-resident kernels
 // of mdp_grads_r.hip serve H = 64 with <= 3 target actors.
 //
-// One 512-thread workgroup (8 waves) owns 16 batch rows; the reduction over
+// One 1024-thread workgroup (16 waves) owns 16 batch rows; the reduction over
 // the batch happens in k_reduce_apply from per-workgroup partials
-// (deterministic).  Every dense layer is spread over ALL waves as 16-column
-// MFMA tiles (fwd_tile / dgrad_tile_relu, weights streamed from L2 in 64-deep
-// chunks with the next chunk in flight); the tiles of independent nets of one
-// phase are dealt round-robin over the waves with no barrier between nets, so
-// a wave's load latency is covered by the other wave on its SIMD.  (The
+// (deterministic).  Every dense layer is spread over ALL 16 waves as MFMA
+// tiles with the next weight chunk in flight: single-net layers as 16-column
+// tiles (fwd_tile / dgrad_tile_relu), the phases of independent nets (target
+// actors + critic) as 64-column groups fed by 16-byte weight loads
+// (fwd_phase_grouped), dealt round-robin over the waves with no barrier
+// between nets, so a wave's load latency is covered by the other waves on its
+// SIMD (4 per SIMD at 1024 threads).  (The
 // earlier design ran one whole net per wave: at H = 128 a wave then waited on
 // ~600 MFMAs and every weight chunk in turn -- the target critic alone took
 // 21 us of a 98 us critic step.)
@@ -57,56 +59,92 @@ __device__ __forceinline__ void fwd_tile(const float* X, int ldx, int K, const f
   }
 }
 
-// A layer phase: the 16-column tiles of several dense layers Y = relu(X W + b)
-// (all N = H wide), dealt round-robin over the waves.  Each wave walks its
-// (tile, 64-deep chunk) items in order with the NEXT item's weight chunk in
-// flight -- across tile boundaries too, so the weight-load latency of a wave's
-// next tile hides behind the current tile's MFMAs.  Job q -> (X, K, W, b, Y)
-// comes from `job`, as LDS offsets and global pointers.
+// A layer phase: several dense layers Y = relu(X W + b) (all N = H wide) of
+// independent nets, dealt over the waves (fwd_phase_grouped).  Job q -> (X, K,
+// W, b, Y) comes from `job`, as LDS offsets and global pointers.
 struct TileJob {
   int xoff, ldx, K;   // X = lds + xoff
   const float* W;     // [K][N] global
   const float* b;
   int yoff;           // Y = lds + yoff (row stride ldy)
 };
+// Unit (job, g) owns output columns
+// 64 g .. 64 g + 63 as 4 MFMA tiles with a permuted column map (tile t, lane
+// column r <-> column 64 g + 4 r + t), so ONE 16-byte load per lane and k-row
+// feeds all 4 tiles: 4x fewer load instructions and 4x the MFMAs per byte in
+// flight of the 16-column version.  Units are dealt round-robin over the
+// waves; each walks its 4 KS-deep k-steps per chunk with the next chunk (of
+// this unit or of the wave's next unit) in flight.
+template <int KS>
+__device__ __forceinline__ void rg_load(f32x4 (&w)[KS], const float* __restrict__ W, int N, int col4, int c0, int K,
+                                        int kq) {
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = c0 + 4 * s + kq;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(W + (int64_t)min(k, K - 1) * N + col4);
+    w[s] = k < K ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+template <int KS>
+__device__ __forceinline__ void rg_acc(f32x4 (&acc)[4], const float* X, int ldx, int r, int c0, int K, int kq,
+                                       const f32x4 (&w)[KS]) {
+  float x[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) x[s] = X[r * ldx + min(c0 + 4 * s + kq, K - 1)];
+  __builtin_amdgcn_sched_barrier(0);  // every A read ahead of the MFMA chain
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (c0 + 4 * s < K) {  // wave-uniform
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s][t], acc[t], 0, 0, 0);
+    }
+  }
+}
 template <class JobFn>
-__device__ __forceinline__ void fwd_phase_pipelined(float* lds, int njobs, int N, int ldy, JobFn job) {
+__device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, int ldy, JobFn job) {
+  constexpr int KS = 8;  // k-steps (of 4) per chunk
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
-  const int r = lane & 15, kq = lane >> 4, ntl = N >> 4, total = njobs * ntl;
-  int t = wave;
-  if (t >= total) return;
-  TileJob j = job(t / ntl);
-  int col = (t % ntl) * 16 + r, c0 = 0;
-  float wa[MDP_KC], wb[MDP_KC];
-  load_wchunk(wa, j.W, N, col, 0, j.K, kq);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int r = lane & 15, kq = lane >> 4, ngr = N >> 6, total = njobs * ngr;
+  int u = wave;
+  if (u >= total) return;
+  TileJob j = job(u / ngr);
+  int g = u % ngr, c0 = 0;
+  f32x4 wa[KS], wb[KS];
+  rg_load<KS>(wa, j.W, N, 64 * g + 4 * r, 0, j.K, kq);
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   while (true) {
-    int t2 = t, c2 = c0 + 4 * MDP_KC, col2 = col;
+    int u2 = u, c2 = c0 + 4 * KS, g2 = g;
     TileJob j2 = j;
-    if (c2 >= j.K) {  // next tile of this wave
-      t2 = t + nw;
+    if (c2 >= j.K) {  // next unit of this wave
+      u2 = u + nw;
       c2 = 0;
-      if (t2 < total) {
-        j2 = job(t2 / ntl);
-        col2 = (t2 % ntl) * 16 + r;
+      if (u2 < total) {
+        j2 = job(u2 / ngr);
+        g2 = u2 % ngr;
       }
     }
-    const bool more = t2 < total;
-    if (more) load_wchunk(wb, j2.W, N, col2, c2, j2.K, kq);
-    acc = mfma_chunk(acc, wa, lds + j.xoff, j.ldx, r, c0, j.K, kq);
-    if (c0 + 4 * MDP_KC >= j.K) {  // tile done
-      const float bias = j.b[col];
-      float* Y = lds + j.yoff;
+    const bool more = u2 < total;
+    if (more) rg_load<KS>(wb, j2.W, N, 64 * g2 + 4 * r, c2, j2.K, kq);
+    rg_acc<KS>(acc, lds + j.xoff, j.ldx, r, c0, j.K, kq, wa);
+    if (c0 + 4 * KS >= j.K) {  // unit done: bias, ReLU, scatter the 4 tiles' columns
+      const f32x4 bias = *reinterpret_cast<const f32x4*>(j.b + 64 * g + 4 * r);
+      float* Y = lds + j.yoff + 64 * g + 4 * r;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Y[(kq * 4 + i) * ldy + col] = fmaxf(acc[i] + bias, 0.f);
-      acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) Y[(kq * 4 + i) * ldy + t] = fmaxf(acc[t][i] + bias[t], 0.f);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     if (!more) break;
 #pragma unroll
-    for (int s2 = 0; s2 < MDP_KC; ++s2) wa[s2] = wb[s2];
-    t = t2;
+    for (int s2 = 0; s2 < KS; ++s2) wa[s2] = wb[s2];
+    u = u2;
     c0 = c2;
-    col = col2;
+    g = g2;
     j = j2;
   }
 }
@@ -211,7 +249,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     const int nj = ng + (g0 == 0 ? 1 : 0);
     const int o_row = (int)(rowbuf - lds), o_xc = (int)(Xc - lds), o_ha = (int)(hA - lds), o_hb = (int)(hB - lds);
     for (int layer = 0; layer < 2; ++layer) {
-      fwd_phase_pipelined(lds, nj, H, ldh, [&](int jb) {
+      fwd_phase_grouped(lds, nj, H, ldh, [&](int jb) {
         const bool actor = jb < ng;
         const ADesc& aj = T.ag[lq ? a.agent : g0 + jb];
         const NDesc& net = actor ? aj.actor : nd;
