@@ -121,6 +121,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
   const ApplyArgs& a = f.ap;
   __shared__ f32x4 red[16][64];
   const int tid = threadIdx.x, lane = tid & 63;
+  MDP_STAMP(30);
   if (f.phase == 1 && b >= f.rblk[6]) return;  // reduce-only pass: chunk workgroups only
   if (b < f.rblk[6]) {
     int t = 0;
@@ -148,17 +149,23 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       if (grp == 0 && act) s = ld4(a.grad + i0);
     } else if (act) {
       const float* base = a.slab + (td.off - a.net.off) + p0;
-      f32x4 v[4];
+      // partials w = grp + 16 k: up to 16 loads (B <= 4096) in flight at once,
+      // summed in the fixed order ((v0 + v1) + v2) + v3, then v4, v5, ...
+      f32x4 v[16];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < 16; ++k) {
         const int w = grp + 16 * k;
         v[k] = w < a.nwg ? ld4(base + (int64_t)w * a.slab_stride) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
       s = ((v[0] + v[1]) + v[2]) + v[3];
-      for (int w = grp + 64; w < a.nwg; w += 16) s += ld4(base + (int64_t)w * a.slab_stride);
+#pragma unroll
+      for (int k = 4; k < 16; ++k)
+        if (grp + 16 * k < a.nwg) s += v[k];
+      for (int w = grp + 256; w < a.nwg; w += 16) s += ld4(base + (int64_t)w * a.slab_stride);
     }
     red[grp][col] = s;
     __syncthreads();
+    MDP_STAMP(31);
     if (grp == 0) {
       f32x4 g = red[0][col];
 #pragma unroll
@@ -197,6 +204,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
+        MDP_STAMP(32);
         tot = 0.0;
         for (int q = lane; q < nch; q += 64) tot += ld_agent(part + q);
         tot = wave_sum_d(tot);
@@ -269,6 +277,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       a.stats_out[1] = -s0 / a.B + (double)a.reg * (s1 / ((double)a.B * MDP_ACT_DIM));
     }
   }
+  MDP_STAMP(33);
   if (f.phase == 1) return;  // uniform: the whole grid of a reduce-only pass
   // the last workgroup to finish advances the optimizer step (every net
   // workgroup read beta before its add, so nobody reads the new values here)
@@ -314,3 +323,10 @@ hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce_apply_batch, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
   return hipGetLastError();
 }
+
+#ifdef MDP_STAMPS
+// diagnostic build: stamps of this translation unit's kernels (own code object)
+extern "C" int mdp_debug_stamps_ra(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif

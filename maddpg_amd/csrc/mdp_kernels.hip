@@ -163,13 +163,21 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs a) {
   float s = 0.f;
   if (el < a.size) {
     const float* p = a.slab + el;
-    float v[8];
+    float v[8], t[24];  // up to 32 partials per lane (B <= 4096) in flight at once
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int w = q + 8 * k;
       v[k] = w < a.nwg ? p[(int64_t)w * a.slab_stride] : 0.f;
     }
-    for (int w = q + 64; w < a.nwg; w += 8) s += p[(int64_t)w * a.slab_stride];
+#pragma unroll
+    for (int k = 0; k < 24; ++k) {
+      const int w = q + 64 + 8 * k;
+      t[k] = w < a.nwg ? p[(int64_t)w * a.slab_stride] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 24; ++k)
+      if (q + 64 + 8 * k < a.nwg) s += t[k];
+    for (int w = q + 256; w < a.nwg; w += 8) s += p[(int64_t)w * a.slab_stride];
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += v[k];
   }

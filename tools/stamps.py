@@ -69,3 +69,13 @@ for lo, hi in seq:
         print(f"{names.get(i, i):>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us  (t={(st[i] - st[lo]) * 10 / 1000:6.2f})")
         prev = st[i]
     print()
+lib_ra = getattr(lib, "mdp_debug_stamps_ra", None)
+if lib_ra is not None:
+    lib_ra.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    rb = (ctypes.c_ulonglong * 64)()
+    lib_ra(rb, 64)
+    ra = np.array(rb[:], dtype=np.int64)
+    if ra[30]:
+        print("k_reduce_apply wg 0 (last launch): partial loads + combine %.2f us, norm handshake %.2f us, "
+              "clip/Adam/stores %.2f us" % ((ra[31] - ra[30]) * 10 / 1000, (ra[32] - ra[31]) * 10 / 1000,
+                                            (ra[33] - ra[32]) * 10 / 1000))
