@@ -276,7 +276,7 @@ struct mdp_handle {
   // single-GPU optimizer step as one k_reduce_apply launch (MDP_UNFUSED_APPLY=1: k_reduce + k_apply)
   bool fused_apply = true;
   uint32_t* ra_ctr = nullptr;
-  double* ra_part = nullptr;
+  uint64_t* ra_part = nullptr;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
   // mdp_train_step graphs (rollout + k rounds), one per k
@@ -543,7 +543,7 @@ FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net) {
   const int g = agent * 2 + net;
   f.sync_ctr = h->ra_ctr + (int64_t)g * 8 * 32;
   f.done_ctr = f.sync_ctr + 6 * 32;
-  f.sync_part = h->ra_part + (int64_t)g * 6 * MDP_RA_MAXCH;
+  f.sync_part = h->ra_part + (int64_t)g * 6 * MDP_RA_MAXCH * 2;
   f.phase = 0;
   f.xd = nullptr;
   f.net_id = g;
@@ -930,7 +930,7 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     p += 8 * na * (int64_t)cfg->batch_size + 256;
     p = (char*)(((uintptr_t)p + 255) & ~uintptr_t(255));
     h->ra_ctr = (uint32_t*)p;
-    h->ra_part = (double*)(p + (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128);
+    h->ra_part = (uint64_t*)(p + (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128);
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
   std::vector<float> beta(8 * cfg->n_agents);

@@ -9,11 +9,12 @@
 // 64 threads each sum a quarter-ish of the per-workgroup partial gradients of
 // the chunk (float4 columns), combined in LDS in a fixed order (deterministic).
 // clip_by_norm needs the norm of the WHOLE tensor (tf_util.py:177-182): every
-// chunk publishes its fp64 sum of squares with an agent-scope store, drains it
-// and bumps the tensor's counter; all chunks of the tensor wait for the counter
-// and sum the published partials in chunk order, so every chunk derives the
-// identical norm.  Counters grow monotonically (target = next multiple of the
-// chunk count, from the value the add returned), so they never need a reset.
+// chunk publishes its fp64 sum of squares as two agent-scope 64-bit stores of
+// (epoch << 32 | half of the bits); all chunks of the tensor poll the pairs
+// until both tags carry this step's epoch and sum them in chunk order, so
+// every chunk derives the identical norm.  The epoch (sync counter 7 of the
+// net) is read at the start and advanced by the last workgroup, so the slots
+// never need a reset and a stale pair never carries the awaited tag.
 // The grid (<= a few dozen workgroups) is always co-resident; every spin is
 // bounded and records a fault in Ctl instead of hanging.
 //
@@ -32,6 +33,12 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
 }
 __device__ __forceinline__ double ld_agent(const double* p) {
   return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // a peer that has not arrived after 30 s (s_memrealtime runs at 100 MHz)
@@ -138,6 +145,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     f32x4 m4 = {0.f, 0.f, 0.f, 0.f}, v4 = m4, th4 = m4, tg4 = m4;
     const float b1p = a.beta[0], b2p = a.beta[1];  // this step's powers (advanced at the end)
     const uint32_t ep = f.phase == 3 ? f.xstep[0] + 1u : 0u;  // exchange epoch (advanced at the end)
+    const uint32_t nep = f.sync_ctr[7 * 32] + 1u;                // norm-handshake epoch (advanced at the end)
     if (grp == 0 && act) {
       m4 = ld4(a.m + i0);
       v4 = ld4(a.v + i0);
@@ -186,27 +194,33 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       double tot = ss;
       if (f.phase != 1) {  // phase 1 (data parallel) stops here: the all-reduce follows
       if (nch > 1) {
-        double* part = f.sync_part + t * MDP_RA_MAXCH;
-        uint32_t* ctr = f.sync_ctr + t * 32;
+        // publish this chunk's fp64 sum of squares as two epoch-tagged 64-bit
+        // words (high and low half) -- data and flag in one store, no counter
+        // RMW -- and read every chunk's pair back once both tags carry this
+        // step's epoch (bounded spin -> Ctl::fault = 1)
+        uint64_t* part = f.sync_part + (int64_t)t * MDP_RA_MAXCH * 2;
+        const uint64_t tag = (uint64_t)nep << 32;
         if (lane == 0) {
-          st_agent(part + c, ss);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t target = (prev / (uint32_t)nch + 1u) * (uint32_t)nch;
+          const uint64_t bits = (uint64_t)__double_as_longlong(ss);
+          st_agent64(part + 2 * c, tag | (bits >> 32));
+          st_agent64(part + 2 * c + 1, tag | (bits & 0xffffffffull));
+        }
+        MDP_STAMP(32);
+        tot = 0.0;
+        for (int q = lane; q < nch; q += 64) {
+          uint64_t hi = ld_agent64(part + 2 * q), lo = ld_agent64(part + 2 * q + 1);
           uint32_t it = 0;
-          while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(2);
+          while ((uint32_t)(hi >> 32) != nep || (uint32_t)(lo >> 32) != nep) {
+            __builtin_amdgcn_s_sleep(1);
             if (++it > kSpinLimit) {
               __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               break;
             }
+            hi = ld_agent64(part + 2 * q);
+            lo = ld_agent64(part + 2 * q + 1);
           }
+          tot += __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
         }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        MDP_STAMP(32);
-        tot = 0.0;
-        for (int q = lane; q < nch; q += 64) tot += ld_agent(part + q);
         tot = wave_sum_d(tot);
       }
       if (act) {
@@ -292,6 +306,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       a.beta[1] = p2 * a.b2;
       if (a.bump_ctr) a.ctl->upd_ctr += (uint32_t)a.bump_ctr;
       if (f.phase == 3) f.xstep[0] += 1u;
+      f.sync_ctr[7 * 32] += 1u;
     }
   }
 }

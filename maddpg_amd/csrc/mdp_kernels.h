@@ -121,7 +121,7 @@ struct FusedApplyArgs {
   ApplyArgs ap;         // ap.slab / nwg / slab_stride: the partial gradients
   int rblk[7];          // prefix counts of MDP_RA_CHUNK workgroups per tensor of ap.net
   uint32_t* sync_ctr;   // 6 tensor counters of this (agent, net), 32 words apart
-  double* sync_part;    // [6][MDP_RA_MAXCH] published sums of squares
+  uint64_t* sync_part;  // [6][MDP_RA_MAXCH][2] published sums of squares (epoch-tagged halves)
   uint32_t* done_ctr;   // workgroups finished (last one advances beta)
   int phase;            // 0 reduce + step; 1 reduce into grad[] only; 2 step from grad[] (all-reduced);
                         // 3 reduce, xGMI exchange with every rank (xd), step x ap.scale
@@ -129,9 +129,9 @@ struct FusedApplyArgs {
   int net_id;           // phase 3: 2 * agent + net (epoch counter)
   uint32_t* xstep;      // phase 3: Ctl::xstep[net_id], exchanges done for this net
 };
-// sync area: per (agent, net) 8 counters x 128 B, then [6][MAXCH] doubles
+// sync area: per (agent, net) 8 counters x 128 B (6 done, 7 norm epoch), then [6][MAXCH][2] tagged words
 inline int64_t mdp_ra_sync_bytes() {
-  return (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128 + (int64_t)MDP_MAX_AGENTS * 2 * 6 * MDP_RA_MAXCH * 8;
+  return (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128 + (int64_t)MDP_MAX_AGENTS * 2 * 6 * MDP_RA_MAXCH * 16;
 }
 
 struct RolloutArgs {
