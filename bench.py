@@ -117,17 +117,24 @@ def load_pmc(kernel, config_key):
         return {}
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, threads=1, seconds=None):
+    """the oracle's reference-structured loop on the host: 1 pinned core (the
+    reference's single_threaded_session), or `threads` BLAS threads unpinned"""
+    seconds = args.cpu_seconds if seconds is None else seconds
     env = dict(os.environ)
     for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
-        env[k] = "1"
+        env[k] = str(threads)
     cmd = [sys.executable, "-m", "oracle.train_loop", "--scenario", args.scenario,
-           "--seconds", str(args.cpu_seconds), "--batch-size", str(args.batch_size),
-           "--num-units", str(args.num_units), "--pin-core", "0"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.cpu_seconds * 6 + 120)
+           "--seconds", str(seconds), "--batch-size", str(args.batch_size),
+           "--num-units", str(args.num_units), "--pin-core", "0" if threads == 1 else "-1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=seconds * 6 + 120)
     if r.returncode != 0:
         return {"error": r.stderr[-500:]}
     out = json.loads(r.stdout.strip().splitlines()[-1])
+    if threads != 1:
+        return {"value": round(out["env_steps_per_sec"], 3), "unit": "env-steps/s", "cores": threads,
+                "trainer_updates_per_sec": round(out["trainer_updates_per_sec"], 3),
+                "sample": f"the same loop with {threads} BLAS threads, unpinned, {out['seconds']:.1f} s"}
     return {"value": round(out["env_steps_per_sec"], 3), "unit": "env-steps/s", "cores": 1, "kind": "port",
             "trainer_updates_per_sec": round(out["trainer_updates_per_sec"], 3),
             "sample": (f"oracle/train_loop.py: {args.scenario} N=3, 1 env, batch {args.batch_size}, "
@@ -335,6 +342,9 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
+            # also the host's cores (the box's CPU share, at most 16)
+            out["cpu_baseline"]["all_cores"] = cpu_baseline(args, threads=min(16, os.cpu_count() or 1),
+                                                            seconds=max(5.0, args.cpu_seconds / 2))
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
