@@ -65,7 +65,7 @@ __device__ __forceinline__ void fwd_tile(const float* X, int ldx, int K, const f
 struct TileJob {
   int xoff, ldx, K;   // X = lds + xoff
   const float* W;     // [K][N] global
-  const float* b;
+  const float* b;     // null: store the raw accumulator (a partial sum over K, no bias / ReLU)
   int yoff;           // Y = lds + yoff (row stride ldy)
 };
 // Unit (job, g) owns output columns
@@ -129,12 +129,20 @@ __device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, 
     if (more) rg_load<KS>(wb, j2.W, N, 64 * g2 + 4 * r, c2, j2.K, kq);
     rg_acc<KS>(acc, lds + j.xoff, j.ldx, r, c0, j.K, kq, wa);
     if (c0 + 4 * KS >= j.K) {  // unit done: bias, ReLU, scatter the 4 tiles' columns
-      const f32x4 bias = *reinterpret_cast<const f32x4*>(j.b + 64 * g + 4 * r);
       float* Y = lds + j.yoff + 64 * g + 4 * r;
+      if (j.b) {
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(j.b + 64 * g + 4 * r);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) Y[(kq * 4 + i) * ldy + t] = fmaxf(acc[t][i] + bias[t], 0.f);
+          for (int t = 0; t < 4; ++t) Y[(kq * 4 + i) * ldy + t] = fmaxf(acc[t][i] + bias[t], 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) Y[(kq * 4 + i) * ldy + t] = acc[t][i];
+        }
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -146,6 +154,38 @@ __device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, 
     c0 = c2;
     g = g2;
     j = j2;
+  }
+}
+
+// fwd_tile continued from a partial: Y tile = act(init + X[:, k0:K] W[k0:K, :] + b),
+// init[16][ldi] the raw accumulator of X[:, 0:k0] W[0:k0, :] (same MFMA k order as
+// one chain over 0..K, so the result is bit-identical to fwd_tile)
+template <bool RELU>
+__device__ __forceinline__ void fwd_tile_from(const float* X, int ldx, int k0, int K, const float* __restrict__ W,
+                                              const float* __restrict__ b, int N, const float* init, int ldi,
+                                              float* Y, int ldy, int nt) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int col = nt * 16 + r;
+  f32x4 acc;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = init[(kq * 4 + i) * ldi + col];
+  float wa[MDP_KC], wb[MDP_KC];
+  load_wchunk(wa, W, N, col, k0, K, kq);
+  const float bias = b[col];
+  for (int c0 = k0; c0 < K; c0 += 4 * MDP_KC) {
+    const bool more = c0 + 4 * MDP_KC < K;
+    if (more) load_wchunk(wb, W, N, col, c0 + 4 * MDP_KC, K, kq);
+    acc = mfma_chunk(acc, wa, X, ldx, r, c0, K, kq);
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v = acc[i] + bias;
+    if (RELU) v = fmaxf(v, 0.f);
+    Y[(kq * 4 + i) * ldy + col] = v;
   }
 }
 
@@ -244,12 +284,27 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   // target actors of the group (+ the critic forward with the first group): each
   // layer phase deals every net's 16-column tiles over all waves
   const int nact = lq ? 1 : T.n;
+  // the target critic's obs' part of layer 1 (maddpg.py:86) does not depend on
+  // the target actions: with the first layer-1 phase, raw, into xl (unused by a
+  // MADDPG critic); only the a~ rows remain after the Gumbel sample
+  const bool tpre = !lq && T.sum_obs % 4 == 0 && ldc >= ldh && MDP_R * ldc >= MDP_R * ldh;
   for (int g0 = 0; g0 < nact; g0 += G) {
     const int ng = min(G, nact - g0);
     const int nj = ng + (g0 == 0 ? 1 : 0);
+    const int nj1 = nj + (g0 == 0 && tpre ? 1 : 0);  // layer-1 jobs
     const int o_row = (int)(rowbuf - lds), o_xc = (int)(Xc - lds), o_ha = (int)(hA - lds), o_hb = (int)(hB - lds);
     for (int layer = 0; layer < 2; ++layer) {
-      fwd_phase_grouped(lds, nj, H, ldh, [&](int jb) {
+      fwd_phase_grouped(lds, layer == 0 ? nj1 : nj, H, ldh, [&](int jb) {
+        if (jb == nj) {  // layer 1 only: the target critic's obs' part
+          TileJob j;
+          j.xoff = (int)(xt - lds);
+          j.ldx = ldc;
+          j.K = T.sum_obs;
+          j.W = a.target + nd.t[0].off;
+          j.b = nullptr;
+          j.yoff = (int)(xl - lds);
+          return j;
+        }
         const bool actor = jb < ng;
         const ADesc& aj = T.ag[lq ? a.agent : g0 + jb];
         const NDesc& net = actor ? aj.actor : nd;
@@ -310,7 +365,12 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   // (maddpg.py:186), loss partials, dL/dq = 2(q-y)/B
   {
     const float* P = a.target;
-    for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(xt, ldc, ag.cin, P + nd.t[0].off, P + nd.t[1].off, H, hA, ldh, nt);
+    if (tpre) {
+      for (int nt = wave; nt < NT; nt += nw)
+        fwd_tile_from<true>(xt, ldc, T.sum_obs, ag.cin, P + nd.t[0].off, P + nd.t[1].off, H, xl, ldh, hA, ldh, nt);
+    } else {
+      for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(xt, ldc, ag.cin, P + nd.t[0].off, P + nd.t[1].off, H, hA, ldh, nt);
+    }
     __syncthreads();
     for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(hA, ldh, H, P + nd.t[2].off, P + nd.t[3].off, H, hB, ldh, nt);
     __syncthreads();
