@@ -189,6 +189,74 @@ __device__ __forceinline__ void fwd_tile_from(const float* X, int ldx, int k0, i
   }
 }
 
+// Prefetched single-net layers: `wa` holds the first 64-deep weight chunk of
+// this wave's tile (nt), issued by the caller AHEAD -- before the barrier that
+// precedes the layer, behind heads, Gumbel sampling and TD on other waves -- so
+// the layer starts on weights already in registers instead of paying a round
+// trip after the barrier.  One tile per wave (nt = wave < N / 16).
+__device__ __forceinline__ void pf_load(float (&wa)[MDP_KC], const float* __restrict__ W, int N, int nt, int k0, int K) {
+  const int lane = threadIdx.x & 63;
+  load_wchunk(wa, W, N, nt * 16 + (lane & 15), k0, K, lane >> 4);
+}
+__device__ __forceinline__ void pf_load_t(float (&wa)[MDP_KC], const float* __restrict__ W, int N, int nt) {
+  const int lane = threadIdx.x & 63;
+  load_wchunk_t(wa, W, N, nt * 16 + (lane & 15), 0, N, lane >> 4, true);
+}
+// Y tile = act([init +] X[:, k0:K] W[k0:K, :] + b); init (raw accumulator of the
+// rows before k0, same MFMA k order as one chain) may be null
+template <bool RELU>
+__device__ __forceinline__ void fwd_tile_pf(const float* X, int ldx, int k0, int K, const float* __restrict__ W,
+                                            const float* __restrict__ b, int N, const float* init, int ldi, float* Y,
+                                            int ldy, int nt, float (&wa)[MDP_KC]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int col = nt * 16 + r;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (init) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = init[(kq * 4 + i) * ldi + col];
+  }
+  const float bias = b[col];
+  float wb[MDP_KC];
+  for (int c0 = k0; c0 < K; c0 += 4 * MDP_KC) {
+    const bool more = c0 + 4 * MDP_KC < K;
+    if (more) load_wchunk(wb, W, N, col, c0 + 4 * MDP_KC, K, kq);
+    acc = mfma_chunk(acc, wa, X, ldx, r, c0, K, kq);
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v = acc[i] + bias;
+    if (RELU) v = fmaxf(v, 0.f);
+    Y[(kq * 4 + i) * ldy + col] = v;
+  }
+}
+// dX tile nt = (dY[16][N] @ W^T) masked by Hin > 0, first chunk of W^T in wa
+__device__ __forceinline__ void dgrad_tile_relu_pf(const float* dY, int ldy, int N, const float* __restrict__ W,
+                                                   const float* Hin, int ldh, float* dX, int ldx, int nt,
+                                                   float (&wa)[MDP_KC]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int kk = nt * 16 + r;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float wb[MDP_KC];
+  for (int c0 = 0; c0 < N; c0 += 4 * MDP_KC) {
+    const bool more = c0 + 4 * MDP_KC < N;
+    if (more) load_wchunk_t(wb, W, N, kk, c0 + 4 * MDP_KC, N, kq, true);
+    acc = mfma_chunk(acc, wa, dY, ldy, r, c0, N, kq);
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = kq * 4 + i;
+    dX[row * ldx + kk] = Hin[row * ldh + kk] > 0.f ? acc[i] : 0.f;
+  }
+}
+
 // dX[16][tile nt of K] = (dY[16][N] @ W^T) masked by Hin > 0, W[K][N] global
 __device__ __forceinline__ void dgrad_tile_relu(const float* dY, int ldy, int N, const float* __restrict__ W,
                                                 const float* Hin, int ldh, float* dX, int ldx, int nt) {
@@ -237,6 +305,8 @@ __device__ __forceinline__ void wgrad_tile(const float* X, int ldx, int K, const
 }
 }  // namespace
 
+static_assert(MDP_GEN_THREADS / 64 >= 128 / 16, "one single-net layer tile per wave (pf_load / *_pf)");
+
 template <int H>
 __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   constexpr int NT = H / 16;
@@ -264,6 +334,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   float* h1c = hA + G * S;
   float* h2c = hB + G * S;
   float* qv = lg + G * MDP_R * 8;
+  float pf[MDP_KC];  // this wave's next single-net layer chunk, issued ahead (wave < NT)
   MDP_STAMP(0);
 
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
@@ -365,14 +436,17 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   // (maddpg.py:186), loss partials, dL/dq = 2(q-y)/B
   {
     const float* P = a.target;
-    if (tpre) {
-      for (int nt = wave; nt < NT; nt += nw)
-        fwd_tile_from<true>(xt, ldc, T.sum_obs, ag.cin, P + nd.t[0].off, P + nd.t[1].off, H, xl, ldh, hA, ldh, nt);
-    } else {
-      for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(xt, ldc, ag.cin, P + nd.t[0].off, P + nd.t[1].off, H, hA, ldh, nt);
+    if (wave < NT) {  // (a prefetch of this layer across the layer phases would spill)
+      pf_load(pf, P + nd.t[0].off, H, wave, tpre ? T.sum_obs : 0, ag.cin);
+      fwd_tile_pf<true>(xt, ldc, tpre ? T.sum_obs : 0, ag.cin, P + nd.t[0].off, P + nd.t[1].off, H,
+                        tpre ? xl : nullptr, ldh, hA, ldh, wave, pf);
+      pf_load(pf, P + nd.t[2].off, H, wave, 0, H);
     }
     __syncthreads();
-    for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(hA, ldh, H, P + nd.t[2].off, P + nd.t[3].off, H, hB, ldh, nt);
+    if (wave < NT) {
+      fwd_tile_pf<true>(hA, ldh, 0, H, P + nd.t[2].off, P + nd.t[3].off, H, nullptr, 0, hB, ldh, wave, pf);
+      pf_load_t(pf, a.theta + nd.t[2].off, H, wave);  // the backward's dh1 = d2 W2^T
+    }
     __syncthreads();
   }
   if (wave == 0) {
@@ -434,7 +508,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   MDP_STAMP(4);
   // dh1 tiles then dW2 tiles, dealt over all waves
   for (int t = wave; t < NT + NT * NT; t += nw) {
-    if (t < NT) dgrad_tile_relu(d2, ldh, H, a.theta + nd.t[2].off, h1c, ldh, d1, ldh, t);
+    if (t < NT) dgrad_tile_relu_pf(d2, ldh, H, a.theta + nd.t[2].off, h1c, ldh, d1, ldh, t, pf);
     else wgrad_tile(h1c, ldh, H, d2, ldh, H, slab + nd.t[2].off, t - NT);
   }
   colsum16(d2, ldh, H, slab + nd.t[3].off);
@@ -477,11 +551,16 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   const float* P = a.theta;
   const int cin = ag.cin;
 
+  float pf[MDP_KC];  // this wave's next layer chunk, issued ahead (wave < NT)
+  if (wave < NT) pf_load(pf, P + na.t[0].off, H, wave, 0, ag.obs_dim);
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
   __syncthreads();
   // actor forward on obs_i -> logits p (maddpg.py:39)
-  for (int nt = wave; nt < NT; nt += nw)
-    fwd_tile<true>(rowbuf + ag.obs_off, ldr, ag.obs_dim, P + na.t[0].off, P + na.t[1].off, H, h1a, ldh, nt);
+  if (wave < NT) {
+    fwd_tile_pf<true>(rowbuf + ag.obs_off, ldr, 0, ag.obs_dim, P + na.t[0].off, P + na.t[1].off, H, nullptr, 0, h1a,
+                      ldh, wave, pf);
+    pf_load(pf, P + na.t[2].off, H, wave, 0, H);
+  }
   // critic input with act_input_n[i] = the sample (maddpg.py:48-52): the replay part now
   for (int e = tid; e < MDP_R * cin; e += blockDim.x) {
     const int r = e / cin, c = e - r * cin;
@@ -489,8 +568,10 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
     x[r * ldc + c] = rowbuf[r * ldr + src];
   }
   __syncthreads();
-  for (int nt = wave; nt < NT; nt += nw)
-    fwd_tile<true>(h1a, ldh, H, P + na.t[2].off, P + na.t[3].off, H, h2a, ldh, nt);
+  if (wave < NT) {
+    fwd_tile_pf<true>(h1a, ldh, 0, H, P + na.t[2].off, P + na.t[3].off, H, nullptr, 0, h2a, ldh, wave, pf);
+    pf_load(pf, P + nc.t[0].off, H, wave, 0, cin);
+  }
   __syncthreads();
   if (wave == 0) {
     head_mfma<H / 4>(h2a, ldh, H, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM, lg, 8);
@@ -509,10 +590,15 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   }
   __syncthreads();
   // critic (post-step weights) forward
-  for (int nt = wave; nt < NT; nt += nw) fwd_tile<true>(x, ldc, cin, P + nc.t[0].off, P + nc.t[1].off, H, h1c, ldh, nt);
+  if (wave < NT) {
+    fwd_tile_pf<true>(x, ldc, 0, cin, P + nc.t[0].off, P + nc.t[1].off, H, nullptr, 0, h1c, ldh, wave, pf);
+    pf_load(pf, P + nc.t[2].off, H, wave, 0, H);
+  }
   __syncthreads();
-  for (int nt = wave; nt < NT; nt += nw)
-    fwd_tile<true>(h1c, ldh, H, P + nc.t[2].off, P + nc.t[3].off, H, h2c, ldh, nt);
+  if (wave < NT) {
+    fwd_tile_pf<true>(h1c, ldh, 0, H, P + nc.t[2].off, P + nc.t[3].off, H, nullptr, 0, h2c, ldh, wave, pf);
+    pf_load_t(pf, P + nc.t[2].off, H, wave);  // dh1c = d2 W2c^T
+  }
   __syncthreads();
   // q (loss value, wave 0) ; dL/dq = -1/B ; d2 = dq * W3c masked by h2c > 0
   if (wave == 0) head_mfma<H / 4>(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
@@ -523,7 +609,10 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   }
   __syncthreads();
   // dh1c = d2 @ W2c^T masked by h1c > 0
-  for (int nt = wave; nt < NT; nt += nw) dgrad_tile_relu(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh, nt);
+  if (wave < NT) {
+    dgrad_tile_relu_pf(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh, wave, pf);
+    pf_load_t(pf, P + na.t[2].off, H, wave);  // dh1a = d2a W2a^T, after the softmax backward
+  }
   __syncthreads();
   if (wave == 0) {
     // da[r][k] = sum_h d1[r][h] * W1c[a_in_off + k][h]   (only the a_i input columns)
@@ -589,7 +678,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   __syncthreads();
   // dh1a tiles then dW2a tiles, dealt over all waves
   for (int t = wave; t < NT + NT * NT; t += nw) {
-    if (t < NT) dgrad_tile_relu(d2, ldh, H, P + na.t[2].off, h1a, ldh, d1, ldh, t);
+    if (t < NT) dgrad_tile_relu_pf(d2, ldh, H, P + na.t[2].off, h1a, ldh, d1, ldh, t, pf);
     else wgrad_tile(h1a, ldh, H, d2, ldh, H, slab + na.t[2].off, t - NT);
   }
   colsum16(d2, ldh, H, slab + na.t[3].off);
