@@ -26,6 +26,7 @@
 #include "mdp_kernels.h"
 
 namespace {
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kSpinLimit = 1u << 22;
 
 __device__ __forceinline__ void st_agent(double* p, double v) {
@@ -261,7 +262,20 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
   } else if (a.stats_mode && tid < 64) {
     // stats workgroup (maddpg.py:196), as in k_apply
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    for (int w = tid; w < a.nwg; w += 64) {
+    int w = tid;  // 4 workgroups' records in flight, summed in the sequential order
+    for (; w + 3 * 64 < a.nwg; w += 4 * 64) {
+      f64x4 r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = *reinterpret_cast<const f64x4*>(a.slab_stat + (int64_t)(w + 64 * k) * 8);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s0 += r[k][0];
+        s1 += r[k][1];
+        s2 += r[k][2];
+        s3 += r[k][3];
+      }
+    }
+    for (; w < a.nwg; w += 64) {
       const double* st = a.slab_stat + (int64_t)w * 8;
       s0 += st[0];
       s1 += st[1];
@@ -275,7 +289,18 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       s3 = wave_sum_d(s3);
       const double mean_y = s1 / a.B;
       double dv = 0.0;
-      for (int i = tid; i < a.B; i += 64) {
+      int i = tid;  // 8 loads in flight, summed in the sequential order
+      for (; i + 7 * 64 < a.B; i += 8 * 64) {
+        double yv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) yv[k] = a.y[i + 64 * k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double d = yv[k] - mean_y;
+          dv += d * d;
+        }
+      }
+      for (; i < a.B; i += 64) {
         const double d = a.y[i] - mean_y;
         dv += d * d;
       }
