@@ -27,6 +27,9 @@
 #include "mdp_device.h"
 #include "mdp_kernels.h"
 
+#ifndef MDP_GKS
+#define MDP_GKS 8  // k-steps (of 4) per weight chunk of the grouped layer phases
+#endif
 #ifndef MDP_GEN_THREADS
 #define MDP_GEN_THREADS 1024  // 16 waves: 4 per SIMD to cover the weight-chunk latency
 #endif
@@ -102,7 +105,7 @@ __device__ __forceinline__ void rg_acc(f32x4 (&acc)[4], const float* X, int ldx,
 }
 template <class JobFn>
 __device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, int ldy, JobFn job) {
-  constexpr int KS = 8;  // k-steps (of 4) per chunk
+  constexpr int KS = MDP_GKS;  // k-steps (of 4) per chunk
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
   const int r = lane & 15, kq = lane >> 4, ngr = N >> 6, total = njobs * ngr;
   int u = wave;
