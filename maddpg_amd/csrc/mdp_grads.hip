@@ -30,6 +30,9 @@
 #ifndef MDP_GKS
 #define MDP_GKS 8  // k-steps (of 4) per weight chunk of the grouped layer phases
 #endif
+#ifndef MDP_SPLITK
+#define MDP_SPLITK 1  // max k-slices of the long layer-1 jobs of the critic kernel (<= 1: off; 3 measured: no gain)
+#endif
 #ifndef MDP_GEN_THREADS
 #define MDP_GEN_THREADS 1024  // 16 waves: 4 per SIMD to cover the weight-chunk latency
 #endif
@@ -66,7 +69,8 @@ __device__ __forceinline__ void fwd_tile(const float* X, int ldx, int K, const f
 // independent nets, dealt over the waves (fwd_phase_grouped).  Job q -> (X, K,
 // W, b, Y) comes from `job`, as LDS offsets and global pointers.
 struct TileJob {
-  int xoff, ldx, K;   // X = lds + xoff
+  int xoff, ldx, K;   // X = lds + xoff; k rows k0 .. K-1 of X and W (a split-K slice: k0 > 0 or K short)
+  int k0;
   const float* W;     // [K][N] global
   const float* b;     // null: store the raw accumulator (a partial sum over K, no bias / ReLU)
   int yoff;           // Y = lds + yoff (row stride ldy)
@@ -111,9 +115,9 @@ __device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, 
   int u = wave;
   if (u >= total) return;
   TileJob j = job(u / ngr);
-  int g = u % ngr, c0 = 0;
+  int g = u % ngr, c0 = j.k0;
   f32x4 wa[KS], wb[KS];
-  rg_load<KS>(wa, j.W, N, 64 * g + 4 * r, 0, j.K, kq);
+  rg_load<KS>(wa, j.W, N, 64 * g + 4 * r, c0, j.K, kq);
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -122,10 +126,10 @@ __device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, 
     TileJob j2 = j;
     if (c2 >= j.K) {  // next unit of this wave
       u2 = u + nw;
-      c2 = 0;
       if (u2 < total) {
         j2 = job(u2 / ngr);
         g2 = u2 % ngr;
+        c2 = j2.k0;
       }
     }
     const bool more = u2 < total;
@@ -362,17 +366,56 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   // the target actions: with the first layer-1 phase, raw, into xl (unused by a
   // MADDPG critic); only the a~ rows remain after the Gumbel sample
   const bool tpre = !lq && T.sum_obs % 4 == 0 && ldc >= ldh && MDP_R * ldc >= MDP_R * ldh;
+  // Split-K of the first layer-1 phase: the two long-K jobs -- the critic (K =
+  // cin, 158 at tag N=6) and the target critic's obs' part (K = sum_obs) -- ran
+  // as one unit per 64-column group, a serial chain of ~5 weight chunks (one
+  // round trip each) while the short target-actor units were done at 40 % of
+  // the phase (stamped).  Here each is cut into sc / st slices of its k-steps,
+  // dealt FIRST so they start at t = 0, with raw partials into hB (unused until
+  // the layer-2 phase); the slices are summed in slice order (+ bias, ReLU for
+  // the critic) right after the phase.
+  int sc = 0, st = 0;
+#if MDP_SPLITK > 1
+  {
+    const int kc = (ag.cin + 3) / 4, kt = (T.sum_obs + 3) / 4;  // k-steps
+    sc = min(MDP_SPLITK, (kc + 2 * MDP_GKS - 1) / (2 * MDP_GKS));  // >= 2 chunks per slice
+    st = tpre ? min(MDP_SPLITK, (kt + 2 * MDP_GKS - 1) / (2 * MDP_GKS)) : 0;
+    while (sc + st > G + 1 && sc + st > 0) {
+      if (sc >= st) --sc;
+      else --st;
+    }
+    if (sc + st < 3 || sc < 1 || (tpre && st < 1)) sc = st = 0;  // nothing to gain
+  }
+#endif
+  const bool split = sc > 0;
   for (int g0 = 0; g0 < nact; g0 += G) {
     const int ng = min(G, nact - g0);
     const int nj = ng + (g0 == 0 ? 1 : 0);
-    const int nj1 = nj + (g0 == 0 && tpre ? 1 : 0);  // layer-1 jobs
+    const bool sp = split && g0 == 0;
+    const int nj1 = sp ? sc + st + ng : nj + (g0 == 0 && tpre ? 1 : 0);  // layer-1 jobs
     const int o_row = (int)(rowbuf - lds), o_xc = (int)(Xc - lds), o_ha = (int)(hA - lds), o_hb = (int)(hB - lds);
     for (int layer = 0; layer < 2; ++layer) {
       fwd_phase_grouped(lds, layer == 0 ? nj1 : nj, H, ldh, [&](int jb) {
+        if (sp && layer == 0 && jb < sc + st) {  // a split-K slice, raw into hB slot jb
+          const bool crit = jb < sc;
+          const int q = crit ? jb : jb - sc, ns = crit ? sc : st;
+          const int K = crit ? ag.cin : T.sum_obs, ks = (K + 3) / 4;
+          TileJob j;
+          j.xoff = crit ? o_xc : (int)(xt - lds);
+          j.ldx = crit ? ldX : ldc;
+          j.k0 = 4 * (q * ks / ns);
+          j.K = min(K, 4 * ((q + 1) * ks / ns));
+          j.W = crit ? a.theta + nd.t[0].off : a.target + nd.t[0].off;
+          j.b = nullptr;
+          j.yoff = o_hb + jb * S;
+          return j;
+        }
+        if (sp && layer == 0) jb -= sc + st;  // then the target actors
         if (jb == nj) {  // layer 1 only: the target critic's obs' part
           TileJob j;
           j.xoff = (int)(xt - lds);
           j.ldx = ldc;
+          j.k0 = 0;
           j.K = T.sum_obs;
           j.W = a.target + nd.t[0].off;
           j.b = nullptr;
@@ -385,6 +428,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
         const float* P = actor ? a.target : a.theta;
         const int slot = (actor ? jb : G) * S;
         TileJob j;
+        j.k0 = 0;
         if (layer == 0) {
           j.xoff = actor ? o_row + aj.nobs_off : o_xc;
           j.ldx = actor ? ldr : ldX;
@@ -402,7 +446,23 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
         }
         return j;
       });
+      if (g0 == 0) MDP_STAMPW((layer == 0 ? 16 : 40) + wave);  // per-wave phase end (diagnostic build)
       __syncthreads();
+      if (sp && layer == 0) {  // sum the slices in slice order: critic h1 = relu(sum + b1), obs' part raw
+        const float* b1 = a.theta + nd.t[1].off;
+        for (int e = tid; e < MDP_R * H; e += blockDim.x) {
+          const int r = e / H, c = e - r * H, o = r * ldh + c;
+          float v = hB[o];
+          for (int q = 1; q < sc; ++q) v += hB[q * S + o];
+          h1c[o] = fmaxf(v + b1[c], 0.f);
+          if (st) {
+            float w = hB[sc * S + o];
+            for (int q = 1; q < st; ++q) w += hB[(sc + q) * S + o];
+            xl[o] = w;
+          }
+        }
+        __syncthreads();
+      }
       if (g0 == 0) MDP_STAMP(6 + layer);
     }
     // heads: net jb on wave jb % nw, then the Gumbel-softmax target actions

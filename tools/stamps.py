@@ -41,6 +41,9 @@ if not fast:
     for i in (1, 6, 7, 8, 2, 3, 4, 5):
         print(f"{names[i]:>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us  (t={(st[i] - st[0]) * 10 / 1000:6.2f})")
         prev = st[i]
+    print("per-wave layer-phase ends (us after the gather; L1 waves 0..15 | L2 waves 0..15):")
+    print("  L1:", " ".join(f"{(st[16 + w] - st[1]) * 10 / 1000:5.2f}" for w in range(16)))
+    print("  L2:", " ".join(f"{(st[40 + w] - st[6]) * 10 / 1000:5.2f}" for w in range(16)))
     seq = []
 else:
     names = {0: "start", 1: "B1 gather+weights (w0)", 2: "tgt actor fwd+gumbel (w0)", 3: "critic L1+L2 (w3)",
