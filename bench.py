@@ -303,6 +303,13 @@ def main():
         if pmc.get("mfma_busy_frac") is not None:
             # SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), profiles/<tag>_mfma.csv
             roof["mfma_busy_frac_rocprof"] = round(pmc["mfma_busy_frac"], 5)
+        if pmc.get("avg_ns"):
+            # the committed rocprofv3 --kernel-trace --stats average of the same kernel and
+            # workload: it spans dispatch to completion signal (incl. the ramp and the
+            # end-of-kernel release), the event figure above subtracts an empty pair's cost
+            roof["rocprof_avg_launch_ms"] = round(pmc["avg_ns"] * 1e-6, 6)
+            roof["frac_at_rocprof_duration"] = round(
+                roof["frac"] * roof["avg_launch_ms"] / roof["rocprof_avg_launch_ms"], 6)
         if pmc.get("_source") or pmc:
             roof["pmc_source"] = "profiles/pmc_traffic.json"
     if rank == 0:
