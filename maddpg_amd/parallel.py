@@ -71,6 +71,30 @@ def strict_round(ops, n_agents, world_size, allreduce):
         ops.apply_grad(i, 0, scale)          # clip + Adam + Polyak (maddpg.py:193-194)
 
 
+def throughput_round(ops, n_agents, world_size, allreduce):
+    """One round of the opt-in throughput mode (NOT the reference's
+    order) with ONE all-reduce: every agent's critic gradients (targets from the
+    round-start target actors) and actor gradients (against the round-start
+    critic), the whole gradient region summed over the ranks at once, then every
+    clip + Adam (x 1/G) and Polyak -- oracle.trainer.update_round_throughput on
+    the global batch.  The torch.distributed counterpart of the library's native
+    throughput DP round (reduce pass -> ncclAllReduce -> step pass).
+
+    ops: as strict_round, plus round_grad_view() -> one flat tensor spanning
+    every net's gradient (written by reduce_grad)."""
+    ops.draw_indices()
+    scale = 1.0 / float(world_size)
+    for i in range(n_agents):
+        ops.critic_grad(i)                   # partials of this net, reduced before the next launch
+        ops.reduce_grad(i, 1)
+        ops.actor_grad(i)                    # round-start critic: nothing stepped yet
+        ops.reduce_grad(i, 0)
+    allreduce(ops.round_grad_view())
+    for i in range(n_agents):
+        ops.apply_grad(i, 1, scale)
+        ops.apply_grad(i, 0, scale)          # + Polyak of both nets
+
+
 class EngineOps:
     """strict_round ops on a maddpg_amd Engine (device indices for this rank)."""
 
@@ -100,6 +124,16 @@ class EngineOps:
 
     def apply_grad(self, i, net, scale):
         self.eng.apply_grad(i, net, scale)
+
+    def round_grad_view(self):
+        """every agent's actor + critic gradient: one contiguous span of the GRAD region"""
+        e = self.eng
+        g = e.region("grad")
+        a = e.grad_view(0, 0)
+        z = e.grad_view(e.n - 1, 1)
+        start = (a.data_ptr() - g.data_ptr()) // 4
+        end = (z.data_ptr() - g.data_ptr()) // 4 + z.numel()
+        return g[start:end]
 
 
 def xgmi_handshake(ops, world, rank):

@@ -13,7 +13,7 @@ updates run on the device in the reference's agent order.
 import os
 from . import envs
 from .engine import Engine
-from .parallel import EngineOps, make_allreduce, strict_round
+from .parallel import EngineOps, make_allreduce, strict_round, throughput_round
 
 
 def rounds_due(t_before, t_after, every=100):
@@ -77,6 +77,8 @@ class VecRunner:
     def train_round(self):
         if self.world_size == 1:
             self.eng.update_round()
+        elif getattr(self.eng, "update_mode", "strict") == "throughput":
+            throughput_round(self._ops, self.n, self.world_size, self._allreduce)
         else:
             strict_round(self._ops, self.n, self.world_size, self._allreduce)
         self.rounds += 1

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from maddpg_amd.parallel import make_allreduce, strict_round
+from maddpg_amd.parallel import make_allreduce, strict_round, throughput_round
 from oracle import nets, trainer
 from tests.helpers import synthetic_trainer_case
 
@@ -45,6 +45,18 @@ class OracleOps:
 
     def grad_view(self, i, net):
         return self.flat[(i, net)]
+
+    def round_grad_view(self):
+        """every net's flat gradient as views of ONE tensor (the one all-reduce of a
+        throughput round sums them all in place)"""
+        keys = sorted(self.flat)
+        whole = torch.cat([self.flat[k] for k in keys])
+        s = 0
+        for k in keys:
+            n = self.flat[k].numel()
+            self.flat[k] = whole[s:s + n]
+            s += n
+        return whole
 
     def apply_grad(self, i, net, scale):
         ag = self.agents[i]
@@ -76,7 +88,7 @@ def _batches(c, rows):
     return out
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="strict"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -85,7 +97,8 @@ def _worker(rank, world, port, q):
     rows = slice(rank * B // world, (rank + 1) * B // world)
     agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
     ops = OracleOps(agents, _batches(c, rows), c["u_tgt"][:, :, rows], c["u_act"][:, rows])
-    strict_round(ops, len(dims), world, make_allreduce(None))
+    rnd = strict_round if mode == "strict" else throughput_round
+    rnd(ops, len(dims), world, make_allreduce(None))
     flat = np.concatenate([np.concatenate([a.actor[k].ravel() for k in NAMES] +
                                           [a.critic[k].ravel() for k in NAMES] +
                                           [a.tgt_actor[k].ravel() for k in NAMES] +
@@ -103,19 +116,26 @@ def _free_port():
     return p
 
 
-def test_strict_round_two_ranks_matches_full_batch():
+def _run_ranks(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(2))
+    res = dict(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
     # replicas bit-identical
-    np.testing.assert_array_equal(res[0], res[1])
+    for r in range(1, world):
+        np.testing.assert_array_equal(res[0], res[r])
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_strict_round_ranks_match_full_batch(world):
+    res = _run_ranks(world, "strict")
     # equal to the single-process update on the whole batch (reference order)
     dims, c = _case()
     agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
@@ -140,4 +160,38 @@ def test_strict_round_single_rank_is_update_batch():
     for x, y in zip(a1, a2):
         for k in NAMES:
             np.testing.assert_array_equal(x.actor[k], y.actor[k])
+            np.testing.assert_array_equal(x.tgt_critic[k], y.tgt_critic[k])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_throughput_round_ranks_match_full_batch(world):
+    """throughput mode: ONE all-reduce of every net's gradient per
+    round; the replicas equal oracle.trainer.update_round_throughput on the
+    whole batch"""
+    res = _run_ranks(world, "throughput")
+    dims, c = _case()
+    agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
+    n = len(dims)
+    idx_n = [c["idx"][i][:64] for i in range(n)]
+    trainer.update_round_throughput(agents, c["data"], idx_n, [c["u_tgt"][i] for i in range(n)],
+                                    [c["u_act"][i] for i in range(n)])
+    want = np.concatenate([np.concatenate([a.actor[k].ravel() for k in NAMES] +
+                                          [a.critic[k].ravel() for k in NAMES] +
+                                          [a.tgt_actor[k].ravel() for k in NAMES] +
+                                          [a.tgt_critic[k].ravel() for k in NAMES]) for a in agents])
+    np.testing.assert_allclose(res[0], want, atol=2e-5)
+
+
+def test_throughput_round_single_rank_is_oracle_round():
+    dims, c = _case()
+    n = len(dims)
+    a1 = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
+    a2 = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
+    throughput_round(OracleOps(a1, _batches(c, slice(0, 64)), c["u_tgt"], c["u_act"]), n, 1, lambda t: None)
+    trainer.update_round_throughput(a2, c["data"], [c["idx"][i][:64] for i in range(n)],
+                                    [c["u_tgt"][i] for i in range(n)], [c["u_act"][i] for i in range(n)])
+    for x, y in zip(a1, a2):
+        for k in NAMES:
+            np.testing.assert_array_equal(x.actor[k], y.actor[k])
+            np.testing.assert_array_equal(x.critic[k], y.critic[k])
             np.testing.assert_array_equal(x.tgt_critic[k], y.tgt_critic[k])
