@@ -234,6 +234,57 @@ def test_throughput_mode_round_parity(dims, local_q, B):
     assert all(np.all(np.isfinite(eng.stats(i))) for i in range(n))
 
 
+def test_torch_distributed_throughput_round_parity():
+    """The torch.distributed fallback's throughput round (parallel.throughput_round
+    over EngineOps: per-agent phase launches, ONE all-reduce over
+    EngineOps.round_grad_view, steps x 1/G) against
+    oracle.trainer.update_round_throughput.  The all-reduce stand-in doubles the
+    span in place and G = 2, so a net outside the span would come out halved."""
+    from maddpg_amd.parallel import EngineOps, throughput_round
+    dims, B, L = [18, 18, 18], 512, 3000
+    c = synthetic_trainer_case(dims, B, L, seed=63)
+    n = len(dims)
+    eng = Engine(dims, batch_size=B, capacity=L + 7)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    for i, p in enumerate(c["params"]):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            eng.set_params(i, w, p[w])
+    eng.set_update_mode("throughput")
+    dev = torch.device("cuda")
+    idx = torch.from_numpy(c["idx"]).to(dev)
+    u_tgt = torch.from_numpy(c["u_tgt"]).to(dev)
+    u_act = torch.from_numpy(c["u_act"]).to(dev)
+
+    class Injected(EngineOps):  # the test's indices and uniforms instead of the device streams
+        def draw_indices(self):
+            pass
+
+        def critic_grad(self, i):
+            self.eng.critic_grad(i, idx[i], u_tgt[i])
+
+        def actor_grad(self, i):
+            self.eng.actor_grad(i, idx[i], u_act[i])
+
+    span = []
+
+    def allreduce(t):
+        span.append(t.numel())
+        t.mul_(2.0)
+
+    throughput_round(Injected(eng), n, 2, allreduce)
+    eng.synchronize()
+    assert span == [int(eng.grad_view(n - 1, 1).data_ptr() - eng.grad_view(0, 0).data_ptr()) // 4
+                    + eng.grad_view(n - 1, 1).numel()]
+    agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
+    trainer.update_round_throughput(agents, c["data"], c["idx"], c["u_tgt"], c["u_act"])
+    for i in range(n):
+        for w, ref in (("actor", agents[i].actor), ("critic", agents[i].critic),
+                       ("tgt_actor", agents[i].tgt_actor), ("tgt_critic", agents[i].tgt_critic)):
+            got = eng.get_params(i, w)
+            for k in ref:
+                assert np.max(np.abs(got[k] - ref[k].reshape(got[k].shape))) < 2e-4, (i, w, k)
+
+
 def test_throughput_mode_train_step_graph_equals_eager():
     """mdp_train_step in throughput mode (rollout + k rounds as one graph) is the
     same work as env_step + k x update_round in throughput mode."""
