@@ -853,6 +853,19 @@ __device__ __forceinline__ double sum16(double v) {
 }
 
 // weight-gradient tiles over waves [w0, w0 + wn)
+// partial-gradient slab store (read once by k_reduce_apply on another CU).
+// MDP_NT_SLAB=1 (nontemporal) measured: gradient kernels -0.2 us, k_reduce_apply
+// 4.94 -> 5.33 us, S2 1.3 % slower end to end -- off.
+#ifndef MDP_NT_SLAB
+#define MDP_NT_SLAB 0
+#endif
+__device__ __forceinline__ void slab_st(float* p, float v) {
+#if MDP_NT_SLAB
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 __device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, const float* dY, int ldy, int N,
                                             float* __restrict__ dW, int w0, int wn) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -875,7 +888,7 @@ __device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, cons
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = mt * 16 + kq * 4 + i;
-      if (k < K) dW[k * N + nt * 16 + r] = acc[i];
+      if (k < K) slab_st(dW + k * N + nt * 16 + r, acc[i]);
     }
   }
 }

@@ -46,7 +46,7 @@ __device__ __forceinline__ void colsum64(const float* X, int ldx, float* __restr
   float s = 0.f;
 #pragma unroll
   for (int r = 0; r < MDP_R; ++r) s += X[r * ldx + c];
-  out[c] = s;
+  slab_st(out + c, s);
 }
 
 // dX tile (columns 16 tt .. 16 tt + 15) = (dY @ W^T) masked by Hin > 0
@@ -111,12 +111,12 @@ __device__ __forceinline__ void dw3a_store(const float* gwpart, const float* dl,
   for (int k = 0; k < MDP_ACT_DIM; ++k) {
     const float g = ((gwpart[k * 64 + lane] + gwpart[(MDP_ACT_DIM + k) * 64 + lane]) +
                      gwpart[(2 * MDP_ACT_DIM + k) * 64 + lane]) + gwpart[(3 * MDP_ACT_DIM + k) * 64 + lane];
-    dw3[lane * MDP_ACT_DIM + k] = g;
+    slab_st(dw3 + lane * MDP_ACT_DIM + k, g);
   }
   if (lane < MDP_ACT_DIM) {
     float s = 0.f;
     for (int rr = 0; rr < MDP_R; ++rr) s += dl[rr * 8 + lane];
-    db3[lane] = s;
+    slab_st(db3 + lane, s);
   }
 }
 }  // namespace
@@ -388,8 +388,8 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         sb += dqr;
         d2[rr * LD + lane] = h > 0.f ? dqr * w3c : 0.f;
       }
-      slab[nd.t[4].off + lane] = s;
-      if (lane == 0) slab[nd.t[5].off] = sb;
+      slab_st(slab + nd.t[4].off + lane, s);
+      if (lane == 0) slab_st(slab + nd.t[5].off, sb);
       MDP_STAMPW(7);
     }
     __syncthreads();  // B5
