@@ -71,28 +71,59 @@ __device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc& x, uint32_t* fault, 
     }
   }
   const bool gone = __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  uint64_t t0 = 0;
-  for (int q = 0; q < W; ++q) {
-    f32x4 v = g;
-    if (q != r && act) {
-      uint64_t* src = x.data[r] + (slot_row + q) * x.pt + i0;
+  // every peer's 4 words in flight at once (one round trip for the whole world,
+  // not one per peer), then only the words still missing, again all at once
+  float pv[MDP_XCH_MAXW][4];
+  uint32_t pend = 0;  // bit 4 q + j: word j of peer q not yet carrying this epoch
+#pragma unroll
+  for (int q = 0; q < MDP_XCH_MAXW; ++q) {
+    if (q < W && q != r && act) {
+      const uint64_t* src = x.data[r] + (slot_row + q) * x.pt + i0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        uint64_t w = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        while ((uint32_t)(w >> 32) != ep && !gone) {
-          __builtin_amdgcn_s_sleep(1);
-          if (t0 == 0) t0 = __builtin_amdgcn_s_memrealtime();
-          if (__builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
-            __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          w = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t w = __hip_atomic_load(const_cast<uint64_t*>(src + j), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+        pv[q][j] = __uint_as_float((uint32_t)w);
+        if ((uint32_t)(w >> 32) != ep) pend |= 1u << (4 * q + j);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pv[q][j] = 0.f;
+    }
+  }
+  uint64_t t0 = 0;
+  while (pend != 0u && !gone) {
+    __builtin_amdgcn_s_sleep(1);
+    if (t0 == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
+      __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    uint32_t still = 0;
+#pragma unroll
+    for (int q = 0; q < MDP_XCH_MAXW; ++q) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (pend & (1u << (4 * q + j))) {
+          const uint64_t* src = x.data[r] + (slot_row + q) * x.pt + i0;
+          const uint64_t w = __hip_atomic_load(const_cast<uint64_t*>(src + j), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((uint32_t)(w >> 32) == ep) pv[q][j] = __uint_as_float((uint32_t)w);
+          else still |= 1u << (4 * q + j);
         }
-        v[j] = __uint_as_float((uint32_t)w);
       }
     }
-    s = q == 0 ? v : s + v;
+    pend = still;
+  }
+  // the world's sum in rank order (identical on every rank)
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < MDP_XCH_MAXW; ++q) {
+    if (q < W) {
+      f32x4 v = g;
+      if (q != r && act) v = f32x4{pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
+      s = q == 0 ? v : s + v;
+    }
   }
   return act ? s : g;
 }

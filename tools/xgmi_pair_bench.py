@@ -9,7 +9,7 @@ workload as bench.py (simple_spread, E envs per rank, B=1024) three ways:
 
 xgmi - pair isolates what the exchange adds per step on top of sharing the GPU.
 
-    python tools/xgmi_pair_bench.py [--envs 1024] [--steps 30]
+    python tools/xgmi_pair_bench.py [--envs 1024] [--steps 30] [--ranks 2]
 """
 import argparse
 import json
@@ -72,14 +72,19 @@ def main():
     ap.add_argument("--envs", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--ranks", type=int, default=2, help="rank processes of the pair/xgmi runs (<= 8)")
+    ap.add_argument("--only-shared", action="store_true", help="skip the solo and rccl1 runs")
     a = ap.parse_args()
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     res = {}
-    for kind, world in (("solo", 1), ("rccl1", 1), ("pair", 2), ("xgmi", 2)):
+    runs = [("pair", a.ranks), ("xgmi", a.ranks)]
+    if not a.only_shared:
+        runs = [("solo", 1), ("rccl1", 1)] + runs
+    for kind, world in runs:
         q = ctx.Queue()
         port = _port()
-        # "pair": two world-1 processes at once (no process group)
+        # "pair": `ranks` world-1 processes at once (no process group)
         ps = [ctx.Process(target=_worker, args=(r, 1 if kind == "pair" else world, port, q, kind, a))
               for r in range(world)]
         for p in ps:
