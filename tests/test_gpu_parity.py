@@ -191,6 +191,56 @@ def test_update_parity_general_kernels_forced(monkeypatch, local_q):
     _update_parity([18, 18, 18], B=256, L=1200, seed=27, local_q=local_q)
 
 
+@pytest.mark.parametrize("dims,local_q,B,H", [([18, 18, 18], None, 1024, 64),
+                                              ([8, 10, 10], [True, False, False], 256, 64),
+                                              ([22, 22, 20], None, 256, 128)])
+def test_update_parity_consecutive_rounds(dims, local_q, B, H):
+    """Four consecutive strict-mode rounds (maddpg.py:161-196 per agent, agent
+    order of train.py:160-161), each with fresh injected indices and Gumbel
+    uniforms, vs the oracle carried along the same path.  Covers what one round
+    cannot: Adam moments and beta powers at t = 2..4, targets drifting from
+    Polyak on top of Polyak, later agents' critics reading earlier agents'
+    stepped target actors of the same round.  Tolerances: critic loss 1e-5
+    relative per round; after the last round every parameter within 1e-4
+    absolute (fp32 summation-order noise over four Adam steps; observed on
+    MI355X: 8.9e-7 spread, 8.0e-7 adversary, 7.3e-6 H=128)."""
+    rounds, L = 4, 3000
+    c = synthetic_trainer_case(dims, B, L, seed=71, local_q=local_q, H=H)
+    n = len(dims)
+    eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L + 7)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    for i, p in enumerate(c["params"]):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            eng.set_params(i, w, p[w])
+    agents = [trainer.AgentParams(**copy.deepcopy(p), local_q=c["local_q"][i]) for i, p in enumerate(c["params"])]
+    rng = np.random.default_rng(72)
+    for r in range(rounds):
+        idx = rng.integers(0, L, size=(n, B)).astype(np.int32)
+        u_tgt = rng.uniform(1e-6, 1.0, size=(n, n, B, 5)).astype(np.float32)
+        u_act = rng.uniform(1e-6, 1.0, size=(n, B, 5)).astype(np.float32)
+        for i in range(n):
+            eng.update(i, idx=torch.from_numpy(idx[i]), u_tgt=torch.from_numpy(u_tgt[i]),
+                       u_act=torch.from_numpy(u_act[i]))
+            got = eng.stats(i)
+            want, _ = trainer.update(agents, i, c["data"], idx[i], u_tgt[i], u_act[i])
+            assert abs(got[0] - want[0]) <= 1e-5 * abs(want[0]) + 1e-7, (r, i, got[0], want[0])
+            np.testing.assert_allclose(got[1:], want[1:], rtol=1e-4, atol=1e-5)
+    worst = 0.0
+    for i in range(n):
+        for w, ref in (("actor", agents[i].actor), ("critic", agents[i].critic),
+                       ("tgt_actor", agents[i].tgt_actor), ("tgt_critic", agents[i].tgt_critic)):
+            dev = eng.get_params(i, w)
+            for k in ref:
+                err = float(np.abs(dev[k] - ref[k].reshape(dev[k].shape)).max())
+                worst = max(worst, err)
+                assert err < 1e-4, (i, w, k, err)
+        for net in (0, 1):
+            bp = eng.get_beta_powers(i, net)
+            opt = agents[i].opt_actor if net == 0 else agents[i].opt_critic
+            assert bp[0] == opt.b1p and bp[1] == opt.b2p
+    print(f"{rounds} rounds dims={dims} B={B} H={H}: worst param |diff| = {worst:.3e}")
+
+
 @pytest.mark.parametrize("dims,local_q,B", [([18, 18, 18], None, 1024), ([4], None, 512),
                                             ([8, 10, 10], [True, False, False], 256)])
 def test_throughput_mode_round_parity(dims, local_q, B):
