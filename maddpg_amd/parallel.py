@@ -24,12 +24,19 @@ import torch.distributed as dist
 
 
 def init_process_group_from_env(backend=None):
-    """torchrun-style init (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
+    """torchrun-style init (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT).
+
+    MDP_SHARED_GPU=1 is a rehearsal of the multi-rank path on a 1-GPU box:
+    every rank on cuda:0 and a gloo process group (RCCL refuses two ranks on
+    one device); the data path (xGMI exchange or torch.distributed fallback)
+    is unchanged."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return 1, 0, 0
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    if os.environ.get("MDP_SHARED_GPU", "0") == "1":
+        local, backend = 0, "gloo"
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Rehearsal of bench.py's multi-rank path on a 1-GPU box (run through gpurun
+# from the repo root):  gpurun --timeout 600 -- 'bash tools/shared_gpu_rehearsal.sh r01k'
+# Every rank on cuda:0 with a gloo process group (MDP_SHARED_GPU=1); the exchange
+# is the real one: direct xGMI inside the optimizer kernel, or with
+# MDP_NATIVE_DP=0 the torch.distributed all-reduce path.  Ranks share one GPU, so
+# the rates say nothing about scaling; this checks that the N>1 code path of the
+# driver's command runs to its JSON line.  Stops at the first failure.
+set -e
+TAG=${1:-rehearsal}
+O=gpurun_out/$TAG/shared_gpu
+mkdir -p $O
+export MDP_SHARED_GPU=1
+run() {  # name nproc extra-env...
+  local name=$1 np=$2; shift 2
+  env "$@" timeout -k 10 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $np \
+      --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 200)) \
+      bench.py --gpus $np --steps 10 --warmup 2 > $O/$name.json 2> $O/$name.err
+  echo "$name: $(tail -c 400 $O/$name.json)"
+}
+run xgmi2 2 MDP_DP_XGMI=1
+run xgmi4 4 MDP_DP_XGMI=1
+run torchdist2 2 MDP_NATIVE_DP=0
+echo "rehearsal $TAG done"
