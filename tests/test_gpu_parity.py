@@ -179,6 +179,18 @@ def test_update_parity_tag6_h128():
     _update_parity([22, 22, 22, 22, 20, 20], B=256, L=1500, seed=25, H=128)
 
 
+def test_update_parity_tag6_full_size():
+    # BASELINE configs[4] at its full size: simple_tag N=6 (4 adversaries: obs 22,
+    # 2 good: obs 20; critic input 158), H=128, B=4096 -> 256 gradient workgroups
+    worst = _update_parity([22, 22, 22, 22, 20, 20], B=4096, L=102400, seed=28, H=128)
+    assert worst < 2e-4
+
+
+def test_update_parity_adversary_full_size():
+    # BASELINE configs[3]: 1 DDPG adversary (critic input 13) + 2 MADDPG good agents, B=1024
+    _update_parity([8, 10, 10], B=1024, L=25600, seed=29, local_q=[True, False, False])
+
+
 def test_update_parity_tag4_h64_general_kernels():
     # 4 target actors: outside the register-resident kernels' envelope -> general kernels
     _update_parity([16, 16, 16, 14], B=512, L=2000, seed=26)
