@@ -54,21 +54,29 @@ def _stats(r):
     return np.concatenate([np.asarray(r.eng.stats(i), np.float64) for i in range(r.n)])
 
 
-def _make(identical, rank, **kw):
+# "tag6": BASELINE configs[4]'s topology (simple_tag, 4 adversaries + 2 good,
+# H=128) -> the general gradient kernels with the exchange in the same fused
+# optimizer launch
+CONFIGS = {"spread": dict(scenario="simple_spread"),
+           "tag6": dict(scenario="simple_tag", n_agents=6, scenario_adversaries=4, num_units=128)}
+
+
+def _make(identical, rank, cfg="spread", **kw):
     from maddpg_amd.runner import VecRunner
     # identical: both processes are "rank 0" of the data (same env copies, same
     # index stream); the exchange is still joined as ranks 0 and 1
-    return VecRunner("simple_spread", 64, batch_size=128, capacity=20000, seed=3, train_every=16,
-                     world_size=1, rank=0 if identical else rank, **kw)
+    c = dict(CONFIGS[cfg])
+    return VecRunner(c.pop("scenario"), 64, batch_size=128, capacity=20000, seed=3, train_every=16,
+                     world_size=1, rank=0 if identical else rank, **c, **kw)
 
 
-def _rank_main(rank, world, port, q, mode, identical, graphs):
+def _rank_main(rank, world, port, q, mode, identical, graphs, cfg):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        r = _make(identical, rank)
+        r = _make(identical, rank, cfg)
         r.eng.set_graphs(graphs)
         ok = r.eng.dp_xgmi_init_from_dist(world, rank)
         assert ok, "xGMI exchange could not be set up"
@@ -80,7 +88,7 @@ def _rank_main(rank, world, port, q, mode, identical, graphs):
         st, stats = _state(r), _stats(r)
         ref = ref_stats = None
         if identical and rank == 0:   # the undistributed run of the same data
-            b = _make(True, 0)
+            b = _make(True, 0, cfg)
             b.eng.set_graphs(graphs)
             if mode != "strict":
                 b.eng.set_update_mode(mode)
@@ -97,12 +105,12 @@ def _rank_main(rank, world, port, q, mode, identical, graphs):
         raise
 
 
-def _run(mode, identical, graphs=True, world=2):
+def _run(mode, identical, graphs=True, world=2, cfg="spread"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q, mode, identical, graphs)) for r in range(world)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q, mode, identical, graphs, cfg)) for r in range(world)]
     for p in ps:
         p.start()
     got = {}
@@ -143,3 +151,20 @@ def test_xgmi_four_ranks():
     for r in range(1, 4):
         np.testing.assert_array_equal(got[r][2], got[0][2])
     np.testing.assert_allclose(got[0][2], got[0][4], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("identical", [True, False])
+def test_xgmi_tag6_h128_general_kernels(identical):
+    """configs[4]'s topology (tag N=6, H=128: general gradient kernels, 12
+    optimizer launches per round each carrying its exchange), strict mode:
+    identical data reproduces the single-GPU run bit for bit; sharded data
+    keeps the replicas bit-identical."""
+    got = _run("strict", identical, True, cfg="tag6")
+    np.testing.assert_array_equal(got[0][2], got[1][2])
+    assert np.all(np.isfinite(got[0][2]))
+    if identical:
+        assert sum(got[0][1]) > 0
+        np.testing.assert_array_equal(got[0][2], got[0][4])
+        np.testing.assert_array_equal(got[0][3], got[0][5])
+    else:
+        assert not np.array_equal(got[0][3], got[1][3])

@@ -11,14 +11,17 @@ TAG=${1:-rehearsal}
 O=gpurun_out/$TAG/shared_gpu
 mkdir -p $O
 export MDP_SHARED_GPU=1
-run() {  # name nproc extra-env...
-  local name=$1 np=$2; shift 2
-  env "$@" timeout -k 10 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $np \
+run() {  # name nproc env-assignment [bench args...]
+  local name=$1 np=$2 ev=$3; shift 3
+  env $ev timeout -k 10 240 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $np \
       --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 200)) \
-      bench.py --gpus $np --steps 10 --warmup 2 > $O/$name.json 2> $O/$name.err
+      bench.py --gpus $np --steps 10 --warmup 2 "$@" > $O/$name.json 2> $O/$name.err
   echo "$name: $(tail -c 400 $O/$name.json)"
 }
 run xgmi2 2 MDP_DP_XGMI=1
 run xgmi4 4 MDP_DP_XGMI=1
 run torchdist2 2 MDP_NATIVE_DP=0
+# configs[4]'s topology (general H=128 kernels), 2 ranks over xGMI
+run tag6_xgmi2 2 MDP_DP_XGMI=1 --scenario simple_tag --num-agents 6 --scenario-adversaries 4 \
+    --num-adversaries 4 --num-units 128 --batch-size 4096 --num-envs 4096 --steps 5
 echo "rehearsal $TAG done"
