@@ -91,6 +91,45 @@ def roofline_for(kind, eng, ms_avg):
             "algorithmic_per_launch": by, "avg_launch_ms": ms_avg}
 
 
+def gather_stage(obs_dims, sizes=(1024, 1 << 16, 1 << 20, 1 << 22), iters=20, capacity=1 << 20):
+    """SURVEY 8d's gather-only stage (replay_buffer.py:34-44 sample_index /
+    _encode_sample, the HBM-roofline part of the north_star's fused
+    sample+gather): k_gather_rows through mdp_sample_rows on uniform indices
+    over a full 2^20-row ring, at the training batch and at bandwidth-bound
+    row counts.  Algorithmic bytes per launch = B*row (read) + 4B (indices)
+    + B*row (the gathered rows written out; inside the gradient kernels they
+    go to LDS instead).  Duration: a HIP event pair around every launch on the
+    engine stream (mdp_prof_*, the empty pair's cost subtracted), so host
+    issue gaps between small launches do not count."""
+    from maddpg_amd.engine import Engine
+    eng = Engine(obs_dims, batch_size=1024, capacity=capacity)
+    eng.set_ring(capacity, 0)
+    row_b = eng.row_stride * 4
+    ev = event_overhead_ms(eng.stream)
+    res = []
+    for B in sizes:
+        idx = torch.randint(0, capacity, (B,), dtype=torch.int32, device=eng.device)
+        out = torch.empty((B, eng.row_stride), dtype=torch.float32, device=eng.device)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            eng.sample_rows(idx, out)
+        eng.prof_enable("gather", True)
+        for _ in range(iters):
+            eng.sample_rows(idx, out)
+        eng.synchronize()
+        ms_tot, n = eng.prof_read("gather")
+        eng.prof_enable("gather", False)
+        ms = max(ms_tot / n - ev, 1e-6)
+        by = 2 * B * row_b + 4 * B
+        gbs = by / (ms * 1e-3) / 1e9
+        res.append({"rows": B, "bytes_per_launch": by, "avg_launch_ms": round(ms, 5), "achieved": round(gbs, 1),
+                    "frac": round(gbs / HBM_PEAK_GBS, 4)})
+        del idx, out
+    eng.close()
+    return {"bound": "hbm", "kernel": "k_gather_rows", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "row_bytes": row_b, "ring_rows": capacity, "sizes": res}
+
+
 def event_overhead_ms(stream, pairs=64):
     """elapsed time of an EMPTY start/stop event pair on `stream` (what a bracketing
     pair adds to every measured launch), median of `pairs` samples."""
@@ -168,6 +207,8 @@ def main():
                     help="throughput: SURVEY 8e's round-parallel mode (not the reference's update order)")
     ap.add_argument("--no-throughput-figure", action="store_true",
                     help="skip the secondary throughput-mode measurement of a strict run")
+    ap.add_argument("--no-gather-stage", action="store_true",
+                    help="skip the gather-only stage figure (SURVEY 8d, rank 0 at N=1)")
     args = ap.parse_args()
 
     world, rank, local = init_process_group_from_env()
@@ -347,6 +388,8 @@ def main():
             "roofline": roof,
             "throughput_mode": tp_fig,
         }
+        if world == 1 and not args.no_gather_stage:
+            out["gather_stage"] = gather_stage(r.spec.obs_dims)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
             # also the host's cores (the box's CPU share, at most 16)
