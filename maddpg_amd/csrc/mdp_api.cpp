@@ -292,6 +292,10 @@ struct mdp_handle {
   RaBatch tp_batch;                   // single GPU: reduce + step
   RaBatch tp_reduce, tp_step;         // data parallel: reduce pass, all-reduce, step pass (x 1/G)
   RaBatch tp_xchg;                    // data parallel over xGMI: reduce + exchange + step (x 1/G)
+  // the xGMI batch only when its whole grid is co-resident (every chunk
+  // workgroup spins on its peers' matching chunk); otherwise one launch per net
+  bool tp_xchg_fits = true;
+  std::vector<FusedApplyArgs> tp_xchg_host;
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
   uint64_t* xbuf = nullptr;
@@ -403,9 +407,13 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
   return 0;
 }
 
-int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr) {
+// tp: throughput mode on the general kernels -- this agent's own blocks of
+// partials / stats / TD targets and noise counter upd_ctr + agent (multi = 2
+// marks it; the general kernels take the agent from a.agent, not the grid)
+int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr,
+                   bool tp = false) {
   CriticArgs a;
-  a.multi = 0;
+  a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.pf_ctl = h->ctl;
   a.pf_out = nullptr;
@@ -426,8 +434,13 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.slab_stride = h->L.slab_c;
   a.slab_stat = h->stat_c;
   a.y_out = h->y;
+  if (tp) {
+    a.slab += (int64_t)agent * h->L.nwg * h->L.slab_c;
+    a.slab_stat += (int64_t)agent * h->L.nwg * 8;
+    a.y_out += (int64_t)agent * h->cfg.batch_size;
+  }
   ProfScope p(h, MDP_K_CRITIC_GRAD);
-  if (!h->general_grads && grads_r_ok(h->L.topo, agent)) {
+  if (!tp && !h->general_grads && grads_r_ok(h->L.topo, agent)) {
     if (pf_out) {
       a.pf_out = pf_out;
       a.pf_count = h->cfg.n_agents * h->cfg.batch_size;
@@ -445,9 +458,9 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   return 0;
 }
 
-int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act) {
+int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, bool tp = false) {
   ActorArgs a;
-  a.multi = 0;
+  a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.topo = h->L.topo;
   a.agent = agent;
@@ -463,8 +476,12 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
   a.slab = h->slab_a;
   a.slab_stride = h->L.slab_a;
   a.slab_stat = h->stat_a;
+  if (tp) {
+    a.slab += (int64_t)agent * h->L.nwg * h->L.slab_a;
+    a.slab_stat += (int64_t)agent * h->L.nwg * 8;
+  }
   ProfScope p(h, MDP_K_ACTOR_GRAD);
-  if (!h->general_grads && grads_r_ok(h->L.topo, agent)) {
+  if (!tp && !h->general_grads && grads_r_ok(h->L.topo, agent)) {
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
     return 0;
   }
@@ -699,10 +716,19 @@ int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, 
 // from the round-start parameters (one launch each), then every optimizer
 // step (clip + Adam + Polyak) in one launch.  NOT the reference's order
 // (maddpg.py:188-194, train.py:160-161): labelled, opt-in.
-bool tp_ok(const mdp_handle* h) {
-  if (h->general_grads || !h->fused_apply) return false;
+// the fast kernels serve every agent: all agents' critic (actor) steps in ONE launch
+bool tp_fast(const mdp_handle* h) {
+  if (h->general_grads) return false;
   for (int i = 0; i < h->cfg.n_agents; ++i)
-    if (!grads_r_ok(h->L.topo, i) || !reduce_apply_ok(h, i, 0) || !reduce_apply_ok(h, i, 1)) return false;
+    if (!grads_r_ok(h->L.topo, i)) return false;
+  return true;
+}
+
+// otherwise the general kernels run one launch per agent and step kind
+bool tp_ok(const mdp_handle* h) {
+  if (!h->fused_apply) return false;
+  for (int i = 0; i < h->cfg.n_agents; ++i)
+    if (!reduce_apply_ok(h, i, 0) || !reduce_apply_ok(h, i, 1)) return false;
   return 2 * h->cfg.n_agents <= MDP_RA_BATCH_MAX;
 }
 
@@ -751,6 +777,14 @@ int tp_setup(mdp_handle* h) {
         rb.wg_start[q + 1] = rb.wg_start[q] + mdp_ra_grid(f);
       }
   }
+  h->tp_xchg_host.assign(list.begin() + 6 * n, list.end());
+  {
+    int dev = 0, cus = 0, per_cu = 0;
+    HIPCHK(h, hipGetDevice(&dev));
+    HIPCHK(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIPCHK(h, mdp_ra_batch_occupancy(&per_cu));
+    h->tp_xchg_fits = (int64_t)h->tp_xchg.wg_start[2 * n] <= (int64_t)cus * per_cu;
+  }
   HIPCHK(h, hipMalloc((void**)&h->tp_list, sizeof(FusedApplyArgs) * list.size()));
   HIPCHK(h, hipMemcpy(h->tp_list, list.data(), sizeof(FusedApplyArgs) * list.size(), hipMemcpyHostToDevice));
   for (int ph = 0; ph < 4; ++ph) rbs[ph]->list = h->tp_list + (int64_t)ph * 2 * n;
@@ -764,6 +798,17 @@ int dp_allreduce_all(mdp_handle* h);
 int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
   const int n = h->cfg.n_agents;
   const int64_t nwg = h->L.nwg;
+  if (!tp_fast(h)) {  // general kernels (H = 128, wide critics): 2n gradient launches
+    const int64_t B = h->cfg.batch_size;
+    int rc;
+    // the next round's draws, which the fast critic kernel makes on the side
+    if (pf_out && (rc = launch_make_index(h, (int)(n * B), pf_out))) return rc;
+    for (int i = 0; i < n; ++i)
+      if ((rc = do_critic_grad(h, i, idx + i * B, u_tgt ? u_tgt + i * n * B * MDP_ACT_DIM : nullptr, nullptr, true)))
+        return rc;
+    for (int i = 0; i < n; ++i)
+      if ((rc = do_actor_grad(h, i, idx + i * B, u_act ? u_act + i * B * MDP_ACT_DIM : nullptr, true))) return rc;
+  } else {
   int lds_c = 0;
   for (int i = 0; i < n; ++i) lds_c = std::max(lds_c, lds_critic_r_bytes(h->L.topo, i));
   {
@@ -814,9 +859,14 @@ int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const flo
     ProfScope p(h, MDP_K_ACTOR_GRAD);
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
   }
+  }  // fast kernels
   if (h->p2p) {  // data parallel over xGMI: reduce + exchange + step of every net, one launch
     ProfScope p(h, MDP_K_REDUCE_APPLY);
-    HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_xchg, h->stream));
+    if (h->tp_xchg_fits) {
+      HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_xchg, h->stream));
+    } else {  // e.g. tag N=6 at H=128: ~1,350 chunk workgroups, one launch per net instead
+      for (const FusedApplyArgs& f : h->tp_xchg_host) HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
+    }
     return 0;
   }
   if (h->comm) {  // data parallel: ONE all-reduce of every net's gradient per round
@@ -1423,7 +1473,7 @@ int mdp_set_update_mode(mdp_handle* h, int32_t mode) {
   if (!h) return -1;
   if (mode != 0 && mode != 1) return fail(h, "update mode must be 0 (strict) or 1 (throughput)");
   if (mode == 1) {
-    if (!tp_ok(h)) return fail(h, "throughput mode needs the fast H=64 kernels for every agent");
+    if (!tp_ok(h)) return fail(h, "throughput mode needs the fused optimizer step for every net and <= 8 agents");
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (tp_setup(h)) return -1;
   }

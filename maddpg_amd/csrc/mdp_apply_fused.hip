@@ -390,6 +390,11 @@ hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
   return hipGetLastError();
 }
 
+// co-resident k_reduce_apply_batch workgroups per CU
+hipError_t mdp_ra_batch_occupancy(int* per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_reduce_apply_batch, 1024, 0);
+}
+
 hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce_apply_batch, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
   return hipGetLastError();

@@ -336,7 +336,9 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   const int r0 = blockIdx.x * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const bool lq = ag.local_q != 0;
-  const uint32_t ctr = a.ctl->upd_ctr;
+  // throughput mode (multi > 1: one launch per agent, every agent from the
+  // round-start parameters) draws agent i's noise at upd_ctr + i, as the fast kernels
+  const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)a.agent : 0u);
   const NDesc& nd = ag.critic;
   float* h1c = hA + G * S;
   float* h2c = hB + G * S;
@@ -608,7 +610,9 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   const int r0 = blockIdx.x * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const bool lq = ag.local_q != 0;
-  const uint32_t ctr = a.ctl->upd_ctr;
+  // throughput mode (multi > 1: one launch per agent, every agent from the
+  // round-start parameters) draws agent i's noise at upd_ctr + i, as the fast kernels
+  const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)a.agent : 0u);
   const NDesc& na = ag.actor;
   const NDesc& nc = ag.critic;
   const float* P = a.theta;

@@ -255,6 +255,7 @@ struct RaBatch {
 };
 int mdp_ra_grid(const FusedApplyArgs& f);
 hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s);
+hipError_t mdp_ra_batch_occupancy(int* per_cu);
 // connection probe of the xGMI exchange: nchunk chunks of a rank-tagged
 // pattern through the same exchange code, *bad += mismatching parameters,
 // *fault = 2 when a peer's flag did not arrive in time

@@ -153,13 +153,13 @@ def test_xgmi_four_ranks():
     np.testing.assert_allclose(got[0][2], got[0][4], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("identical", [True, False])
-def test_xgmi_tag6_h128_general_kernels(identical):
-    """configs[4]'s topology (tag N=6, H=128: general gradient kernels, 12
-    optimizer launches per round each carrying its exchange), strict mode:
-    identical data reproduces the single-GPU run bit for bit; sharded data
-    keeps the replicas bit-identical."""
-    got = _run("strict", identical, True, cfg="tag6")
+@pytest.mark.parametrize("mode,identical", [("strict", True), ("strict", False), ("throughput", True)])
+def test_xgmi_tag6_h128_general_kernels(mode, identical):
+    """configs[4]'s topology (tag N=6, H=128: general gradient kernels; strict:
+    12 optimizer launches per round each carrying its exchange, throughput: one
+    batched launch): identical data reproduces the single-GPU run bit for bit;
+    sharded data keeps the replicas bit-identical."""
+    got = _run(mode, identical, True, cfg="tag6")
     np.testing.assert_array_equal(got[0][2], got[1][2])
     assert np.all(np.isfinite(got[0][2]))
     if identical:

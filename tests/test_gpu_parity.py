@@ -253,18 +253,24 @@ def test_update_parity_consecutive_rounds(dims, local_q, B, H):
     print(f"{rounds} rounds dims={dims} B={B} H={H}: worst param |diff| = {worst:.3e}")
 
 
-@pytest.mark.parametrize("dims,local_q,B", [([18, 18, 18], None, 1024), ([4], None, 512),
-                                            ([8, 10, 10], [True, False, False], 256)])
-def test_throughput_mode_round_parity(dims, local_q, B):
+@pytest.mark.parametrize("dims,local_q,B,H,general", [
+    ([18, 18, 18], None, 1024, 64, False), ([4], None, 512, 64, False),
+    ([8, 10, 10], [True, False, False], 256, 64, False),
+    # the general kernels: one gradient launch per agent and step kind
+    ([22, 22, 22, 22, 20, 20], None, 256, 128, False), ([16, 16, 16, 14], None, 256, 64, False),
+    ([8, 10, 10], [True, False, False], 256, 64, True)])
+def test_throughput_mode_round_parity(monkeypatch, dims, local_q, B, H, general):
     """Throughput mode (opt-in): one round = every agent's critic and
     actor gradients from the round-start parameters, then every clip + Adam +
     Polyak (mdp_update_all) vs oracle.trainer.update_round_throughput on the
     same injected indices and uniforms: critic loss within 1e-5 relative,
     parameters within the fp32 tolerance of the strict-mode parity test."""
+    if general:
+        monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
     L = 3000
-    c = synthetic_trainer_case(dims, B, L, seed=61, local_q=local_q)
+    c = synthetic_trainer_case(dims, B, L, seed=61, local_q=local_q, H=H)
     n = len(dims)
-    eng = Engine(dims, c["local_q"], batch_size=B, capacity=L + 7)
+    eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L + 7)
     eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
     for i, p in enumerate(c["params"]):
         for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
@@ -347,13 +353,17 @@ def test_torch_distributed_throughput_round_parity():
                 assert np.max(np.abs(got[k] - ref[k].reshape(got[k].shape))) < 2e-4, (i, w, k)
 
 
-def test_throughput_mode_train_step_graph_equals_eager():
+@pytest.mark.parametrize("cfg", ["spread", "tag6_h128"])
+def test_throughput_mode_train_step_graph_equals_eager(cfg):
     """mdp_train_step in throughput mode (rollout + k rounds as one graph) is the
-    same work as env_step + k x update_round in throughput mode."""
+    same work as env_step + k x update_round in throughput mode (tag6_h128: the
+    general kernels, one gradient launch per agent and step kind)."""
     from maddpg_amd.runner import VecRunner
+    kw = (dict(n_agents=6, scenario_adversaries=4, num_units=128) if cfg == "tag6_h128" else {})
+    scen = "simple_tag" if cfg == "tag6_h128" else "simple_spread"
 
     def make():
-        r = VecRunner("simple_spread", 64, batch_size=128, capacity=20000, seed=3, train_every=16)
+        r = VecRunner(scen, 64, batch_size=128, capacity=20000, seed=3, train_every=16, **kw)
         r.eng.set_update_mode("throughput")
         r.prefill()
         return r
@@ -368,7 +378,8 @@ def test_throughput_mode_train_step_graph_equals_eager():
             b.train_round()
     a.eng.synchronize()
     b.eng.synchronize()
-    for i in range(3):
+    assert a.rounds > 0
+    for i in range(a.n):
         for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_critic", "v_actor"):
             pa, pb = a.eng.get_params(i, w), b.eng.get_params(i, w)
             for key in pa:
