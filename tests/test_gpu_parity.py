@@ -77,6 +77,23 @@ def test_fused_gather_bit_exact_vs_reference(golden, name):
         assert _digest(arrs) == c["sha"][i], f"agent {i}"
 
 
+@pytest.mark.parametrize("dims,rows", [([18, 18, 18], 300_000), ([22, 22, 22, 22, 20, 20], 131_071), ([4], 1)])
+def test_gather_large_batches_bit_exact(dims, rows):
+    """k_gather_rows beyond the golden fixtures' sizes: enough rows that every
+    thread of the capped grid runs the 4-element unrolled loop AND the tail
+    (S2: 300K rows x 33 float4 > 4096 x 256 x 3), an odd count, a single row.
+    A row copy, so bit-exact against indexing the ring on the device."""
+    cap = 1 << 18
+    eng = Engine(dims, batch_size=8, capacity=cap)
+    eng.add_rows(torch.rand(cap, eng.row_stride))
+    idx = torch.randint(0, cap, (rows,), dtype=torch.int32)
+    idx[0], idx[-1] = 0, cap - 1
+    got = eng.sample_rows(idx)
+    ring = eng.region("replay")[:cap * eng.row_stride].view(cap, eng.row_stride)
+    want = ring[idx.to(ring.device).long()]
+    assert torch.equal(got, want)
+
+
 def test_make_index_continues_python_global_state():
     random.seed(99)
     for _ in range(37):
