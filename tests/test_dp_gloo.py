@@ -195,3 +195,35 @@ def test_throughput_round_single_rank_is_oracle_round():
             np.testing.assert_array_equal(x.actor[k], y.actor[k])
             np.testing.assert_array_equal(x.critic[k], y.critic[k])
             np.testing.assert_array_equal(x.tgt_critic[k], y.tgt_critic[k])
+
+
+def _env_init_worker(rank, world, port, shared, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if shared:
+        os.environ["MDP_SHARED_GPU"] = "1"
+    from maddpg_amd.parallel import init_process_group_from_env
+    w, r, local = init_process_group_from_env()
+    t = torch.tensor([float(r + 1)])
+    dist.all_reduce(t)
+    q.put((r, w, local, dist.get_backend(), float(t.item())))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_init_process_group_from_env(shared):
+    """torchrun-style init as bench.py uses it; MDP_SHARED_GPU=1 (the 1-GPU
+    rehearsal of the multi-rank command) puts every rank on device 0 with gloo."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_env_init_worker, args=(r, 2, port, shared, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [g[0] for g in got] == [0, 1] and all(g[1] == 2 for g in got)
+    assert all(g[3] == "gloo" and g[4] == 3.0 for g in got)
+    assert [g[2] for g in got] == ([0, 0] if shared else [0, 1])
