@@ -795,20 +795,11 @@ int dp_allreduce_all(mdp_handle* h);
 
 // every agent's gradients + every optimizer step; idx [n][B]; optional injected
 // uniforms u_tgt [n][n][B][5] (agent, target actor j, row) and u_act [n][B][5]
-int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
+// throughput-mode gradients on the fast kernels: every agent's critic (actor)
+// step in ONE launch, workgroup -> (agent, row tile)
+int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
   const int n = h->cfg.n_agents;
   const int64_t nwg = h->L.nwg;
-  if (!tp_fast(h)) {  // general kernels (H = 128, wide critics): 2n gradient launches
-    const int64_t B = h->cfg.batch_size;
-    int rc;
-    // the next round's draws, which the fast critic kernel makes on the side
-    if (pf_out && (rc = launch_make_index(h, (int)(n * B), pf_out))) return rc;
-    for (int i = 0; i < n; ++i)
-      if ((rc = do_critic_grad(h, i, idx + i * B, u_tgt ? u_tgt + i * n * B * MDP_ACT_DIM : nullptr, nullptr, true)))
-        return rc;
-    for (int i = 0; i < n; ++i)
-      if ((rc = do_actor_grad(h, i, idx + i * B, u_act ? u_act + i * B * MDP_ACT_DIM : nullptr, true))) return rc;
-  } else {
   int lds_c = 0;
   for (int i = 0; i < n; ++i) lds_c = std::max(lds_c, lds_critic_r_bytes(h->L.topo, i));
   {
@@ -859,7 +850,28 @@ int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const flo
     ProfScope p(h, MDP_K_ACTOR_GRAD);
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
   }
-  }  // fast kernels
+  return 0;
+}
+
+// ... and on the general kernels (H = 128, wide critics): 2n gradient launches
+int tp_grads_general(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
+  const int n = h->cfg.n_agents;
+  const int64_t B = h->cfg.batch_size;
+  int rc;
+  // the next round's draws, which the fast critic kernel makes on the side
+  if (pf_out && (rc = launch_make_index(h, (int)(n * B), pf_out))) return rc;
+  for (int i = 0; i < n; ++i)
+    if ((rc = do_critic_grad(h, i, idx + i * B, u_tgt ? u_tgt + i * n * B * MDP_ACT_DIM : nullptr, nullptr, true)))
+      return rc;
+  for (int i = 0; i < n; ++i)
+    if ((rc = do_actor_grad(h, i, idx + i * B, u_act ? u_act + i * B * MDP_ACT_DIM : nullptr, true))) return rc;
+  return 0;
+}
+
+int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
+  const int rc = tp_fast(h) ? tp_grads_fast(h, idx, u_tgt, u_act, pf_out)
+                            : tp_grads_general(h, idx, u_tgt, u_act, pf_out);
+  if (rc) return rc;
   if (h->p2p) {  // data parallel over xGMI: reduce + exchange + step of every net, one launch
     ProfScope p(h, MDP_K_REDUCE_APPLY);
     if (h->tp_xchg_fits) {
