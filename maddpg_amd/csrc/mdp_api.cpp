@@ -295,6 +295,7 @@ struct mdp_handle {
   // the xGMI batch only when its whole grid is co-resident (every chunk
   // workgroup spins on its peers' matching chunk); otherwise one launch per net
   bool tp_xchg_fits = true;
+  bool rollout_draw = true;           // step_launches: first-round draw inside k_rollout
   std::vector<FusedApplyArgs> tp_xchg_host;
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
@@ -935,6 +936,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->general_grads = g && g[0] == '1';
     const char* u = getenv("MDP_UNFUSED_APPLY");
     h->fused_apply = !(u && u[0] == '1');
+    const char* rd = getenv("MDP_ROLLOUT_DRAW");
+    h->rollout_draw = !(rd && rd[0] == '0');
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
@@ -1564,8 +1567,13 @@ int mdp_env_reset(mdp_handle* h) {
   return 0;
 }
 
-static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* u_dev, float* bench = nullptr) {
+// pf_out: an extra rollout workgroup draws pf_count indices for the step's
+// first round against the post-step ring length (the draw leaves the critical path)
+static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* u_dev, float* bench = nullptr,
+                           int32_t* pf_out = nullptr, int pf_count = 0) {
   RolloutArgs a;
+  a.pf_out = pf_out;
+  a.pf_count = pf_out ? pf_count : 0;
   a.topo = h->L.topo;
   a.env = h->L.env;
   a.theta = h->theta;
@@ -1621,12 +1629,14 @@ int mdp_env_step_bench(mdp_handle* h, float* info_dev) {
 // step follow one rollout) in an extra workgroup -- the draw leaves the
 // critical path for every round but the first
 static int step_launches(mdp_handle* h, int rounds) {
-  int rc = env_step_launch(h, nullptr, nullptr);
-  if (rc || rounds == 0) return rc;
   const int nb = h->cfg.n_agents * h->cfg.batch_size;
   int32_t* slot[2] = {h->index, h->index + nb};
+  // the first round's draw rides in the rollout launch (MDP_ROLLOUT_DRAW=0: its own launch)
+  const bool in_rollout = rounds > 0 && h->rollout_draw;
+  int rc = env_step_launch(h, nullptr, nullptr, nullptr, in_rollout ? slot[0] : nullptr, nb);
+  if (rc || rounds == 0) return rc;
   const bool pf = prefetch_ok(h);
-  if ((rc = launch_make_index(h, nb, slot[0]))) return rc;
+  if (!in_rollout && (rc = launch_make_index(h, nb, slot[0]))) return rc;
   for (int r = 0; r < rounds && !rc; ++r) {
     const bool more = r + 1 < rounds;
     rc = round_updates(h, slot[r & 1], (more && pf) ? slot[(r + 1) & 1] : nullptr);

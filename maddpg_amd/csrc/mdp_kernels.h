@@ -154,6 +154,10 @@ struct RolloutArgs {
   const float* u_in;
   uint32_t* ticket;
   float* bench;  // benchmark_data records [E][n][MDP_BENCH_W] or null
+  // > 0: one extra workgroup draws the step's first-round indices (pf_count
+  // randint draws against the ring length after this step) beside the envs
+  int pf_count;
+  int32_t* pf_out;
 };
 
 struct EnvResetArgs {

@@ -677,6 +677,16 @@ __global__ __launch_bounds__(256) void k_env_obs(EnvObsArgs a) {
 }
 
 // One vector env step for 16 env copies per workgroup (train.py:112-128).
+// the last workgroup to arrive advances the ring and the env step counter
+__device__ __forceinline__ void rollout_finish(const RolloutArgs& a, int64_t next, int64_t len) {
+  if (last_block(a.ticket) && threadIdx.x == 0) {
+    a.ctl->next = (next + a.E) % a.cap;
+    a.ctl->len = len + a.E < a.cap ? len + a.E : a.cap;
+    a.ctl->env_steps += 1;
+    *a.ticket = 0u;
+  }
+}
+
 template <int H>
 __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -697,6 +707,15 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   const int nvalid = min(MDP_R, a.E - e0);
   const int64_t next = a.ctl->next, len = a.ctl->len;
   const uint32_t step = (uint32_t)a.ctl->env_steps;
+  if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
+    // the index draw of the step's first round, off the critical path: the
+    // MT state is untouched by the env workgroups, and the length is the one
+    // the last workgroup below will store (every workgroup read ctl->len
+    // before arriving at the ticket)
+    make_index_block<MDP_NT>(a.ctl, a.pf_count, a.pf_out, (uint32_t)(len + a.E < a.cap ? len + a.E : a.cap));
+    rollout_finish(a, next, len);
+    return;
+  }
 
   for (int q = tid; q < MDP_R * 2 * ne; q += MDP_NT) {
     const int r = q / (2 * ne), c = q - r * 2 * ne;
@@ -796,12 +815,7 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     a.pos[(int64_t)(e0 + r) * 2 * ne + c] = sp[r * 2 * MDP_MAX_ENT + c];
     a.vel[(int64_t)(e0 + r) * 2 * ne + c] = sv[r * 2 * MDP_MAX_ENT + c];
   }
-  if (last_block(a.ticket) && tid == 0) {
-    a.ctl->next = (next + a.E) % a.cap;
-    a.ctl->len = len + a.E < a.cap ? len + a.E : a.cap;
-    a.ctl->env_steps += 1;
-    *a.ticket = 0u;
-  }
+  rollout_finish(a, next, len);
 }
 
 // batched policy / critic evaluation for the facade (action, target_act, q_values)
@@ -849,7 +863,7 @@ __global__ __launch_bounds__(MDP_NT) void k_mlp_eval(EvalArgs a) {
 
 template <int H>
 static hipError_t launch_rollout_t(const RolloutArgs& a, int lds_bytes, hipStream_t s) {
-  const int grid = (a.E + MDP_R - 1) / MDP_R;
+  const int grid = (a.E + MDP_R - 1) / MDP_R + (a.pf_count > 0 ? 1 : 0);
   hipLaunchKernelGGL(k_rollout<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
   MDP_CHECK_LAUNCH();
   return hipSuccess;

@@ -77,15 +77,18 @@ __device__ __forceinline__ void mt_twist(uint32_t* mt) {
 
 // count draws of randint(0, ctl->len - 1) into out[], advancing ctl's state.
 // Must be called by all NT threads of the workgroup (blockDim.x == NT).
+// len_override > 0: draw from randint(0, len_override - 1) instead of ctl->len
+// (k_rollout's extra workgroup draws against the length its step leaves).
 template <int NT>
-__device__ __forceinline__ void make_index_block(Ctl* ctl, int count, int32_t* __restrict__ out) {
+__device__ __forceinline__ void make_index_block(Ctl* ctl, int count, int32_t* __restrict__ out,
+                                                 uint32_t len_override = 0u) {
   __shared__ uint32_t mt[624];
   __shared__ int wsum[NT / 64];
   __shared__ int s_newpos;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   for (int i = t; i < 624; i += NT) mt[i] = ctl->mt[i];
   int pos = ctl->mt_pos;
-  const uint32_t n = (uint32_t)ctl->len;
+  const uint32_t n = len_override ? len_override : (uint32_t)ctl->len;
   if (n == 0) {  // randint(0, -1) raises in the reference; the host refuses it too
     for (int i = t; i < count; i += NT) out[i] = 0;
     return;

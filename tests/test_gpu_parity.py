@@ -562,13 +562,17 @@ def test_rollout_policy_actions_match_oracle():
         np.testing.assert_allclose(rows[:, lay[j]["act"]:lay[j]["act"] + ACT], want, atol=2e-6)
 
 
-def test_train_step_graph_equals_step_then_rounds():
-    """mdp_train_step(k) (rollout + k rounds replayed as one graph) is the same
-    work as env_step + k x update_round: bit-identical state after 4 steps."""
+@pytest.mark.parametrize("cap", [20000, 3300])
+def test_train_step_graph_equals_step_then_rounds(cap):
+    """mdp_train_step(k) (rollout + k rounds replayed as one graph; the first
+    round's indices drawn by an extra rollout workgroup) is the same work as
+    env_step + k x update_round: bit-identical state and RNG stream after 4
+    steps.  cap=3300: the ring fills during the steps (draws against the
+    capped length)."""
     from maddpg_amd.runner import VecRunner
 
     def make():
-        r = VecRunner("simple_spread", 64, batch_size=128, capacity=20000, seed=3, train_every=16)
+        r = VecRunner("simple_spread", 64, batch_size=128, capacity=cap, seed=3, train_every=16)
         r.prefill()
         return r
 
@@ -590,6 +594,7 @@ def test_train_step_graph_equals_step_then_rounds():
                 np.testing.assert_array_equal(pa[key], pb[key])
     np.testing.assert_array_equal(a.eng.replay_rows(0, 2000).cpu().numpy(), b.eng.replay_rows(0, 2000).cpu().numpy())
     assert a.eng.buffer_len() == b.eng.buffer_len()
+    np.testing.assert_array_equal(a.eng.get_rng_state(), b.eng.get_rng_state())
 
 
 # ---------------------------------------------------- size-independent checks
