@@ -19,6 +19,7 @@ import subprocess
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -156,14 +157,15 @@ def load_pmc(kernel, config_key):
         return {}
 
 
-def cpu_baseline(args, threads=1, seconds=None):
+def cpu_baseline(args, threads=1, seconds=None, scenario=None):
     """the oracle's reference-structured loop on the host: 1 pinned core (the
     reference's single_threaded_session), or `threads` BLAS threads unpinned"""
     seconds = args.cpu_seconds if seconds is None else seconds
+    scenario = scenario or args.scenario
     env = dict(os.environ)
     for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
         env[k] = str(threads)
-    cmd = [sys.executable, "-m", "oracle.train_loop", "--scenario", args.scenario,
+    cmd = [sys.executable, "-m", "oracle.train_loop", "--scenario", scenario,
            "--seconds", str(seconds), "--batch-size", str(args.batch_size),
            "--num-units", str(args.num_units), "--pin-core", "0" if threads == 1 else "-1"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=seconds * 6 + 120)
@@ -176,11 +178,42 @@ def cpu_baseline(args, threads=1, seconds=None):
                 "sample": f"the same loop with {threads} BLAS threads, unpinned, {out['seconds']:.1f} s"}
     return {"value": round(out["env_steps_per_sec"], 3), "unit": "env-steps/s", "cores": 1, "kind": "port",
             "trainer_updates_per_sec": round(out["trainer_updates_per_sec"], 3),
-            "sample": (f"oracle/train_loop.py: {args.scenario} N=3, 1 env, batch {args.batch_size}, "
+            "sample": (f"oracle/train_loop.py: {scenario} N={out.get('n_agents', '?')}, 1 env, batch {args.batch_size}, "
                        f"{args.num_units}-unit MLPs, reference call structure (batch-1 action per agent, "
                        f"Python-list replay, sequential per-agent updates every 100 steps), numpy fp32 on "
                        f"1 pinned core, replay prefilled to the gate; {out['env_steps']} env steps + "
                        f"{out['updates']} updates in {out['seconds']:.1f} s")}
+
+
+def configs2_per_gpu(args, steps=12, warmup=3):
+    """BASELINE configs[2]'s per-GPU share on this GPU: simple_spread N=3 with
+    4096 env copies, batch 1024, the same cadence (41 update rounds per vector
+    step); the multi-GPU runs use this E per rank"""
+    E = 4096
+    r = VecRunner(args.scenario, E, n_agents=args.num_agents, scenario_adversaries=args.scenario_adversaries,
+                  num_adversaries=args.num_adversaries, good_policy=args.good_policy, adv_policy=args.adv_policy,
+                  batch_size=args.batch_size, num_units=args.num_units, seed=args.seed + 1,
+                  train_every=args.train_every)
+    r.prefill()
+    for _ in range(warmup):
+        r.step()
+    r.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rounds = 0
+    for _ in range(steps):
+        rounds += r.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    r.synchronize()
+    finite = all(bool(np.isfinite(v).all()) for i in range(r.n) for v in r.eng.get_params(i, "critic").values())
+    out = {"env_steps_per_sec": round(E * steps / dt, 3), "trainer_updates_per_sec": round(rounds * r.n / dt, 3),
+           "rounds_per_sec": round(rounds / dt, 3), "ms_per_step": round(dt / steps * 1e3, 4), "steps": steps,
+           "num_envs": E, "params_finite": finite,
+           "note": "configs[2] per-GPU workload (4096 simple_spread copies per GPU) on 1 GPU; "
+                   "the N>1 bench lines run exactly this per rank"}
+    r.eng.close()
+    return out
 
 
 def main():
@@ -189,7 +222,8 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scenario", default="simple_spread")
-    ap.add_argument("--num-envs", type=int, default=1024)
+    ap.add_argument("--num-envs", type=int, default=None,
+                    help="env copies per GPU (default: 1024 = configs[1] at N=1, 4096 = configs[2] at N>1)")
     ap.add_argument("--batch-size", type=int, default=1024)
     ap.add_argument("--num-units", type=int, default=64)
     ap.add_argument("--train-every", type=int, default=100)
@@ -207,6 +241,8 @@ def main():
                     help="throughput: SURVEY 8e's round-parallel mode (not the reference's update order)")
     ap.add_argument("--no-throughput-figure", action="store_true",
                     help="skip the secondary throughput-mode measurement of a strict run")
+    ap.add_argument("--no-configs2", action="store_true",
+                    help="skip the 4096-envs-per-GPU figure (BASELINE configs[2]) of an N=1 run")
     ap.add_argument("--no-gather-stage", action="store_true",
                     help="skip the gather-only stage figure (SURVEY 8d, rank 0 at N=1)")
     args = ap.parse_args()
@@ -214,6 +250,8 @@ def main():
     world, rank, local = init_process_group_from_env()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.num_envs is None:   # BASELINE configs[1] on one GPU, configs[2] across GPUs
+        args.num_envs = 1024 if world == 1 else 4096
     torch.cuda.set_device(local)
     r = VecRunner(args.scenario, args.num_envs, n_agents=args.num_agents,
                   scenario_adversaries=args.scenario_adversaries, num_adversaries=args.num_adversaries,
@@ -251,6 +289,20 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    dp_check = None
+    if world > 1:
+        # the run validates itself: every rank's ms/step, the communicator the
+        # exchange ran over, and bit-identical replicas (strict data parallelism
+        # keeps every rank's weights, targets, Adam moments and beta powers equal)
+        r.synchronize()
+        info = {"ms_per_step": round(dt / args.steps * 1e3, 4), "checksum": eng.param_checksum(),
+                "dp": eng.dp_info() if getattr(r, "native_dp", False) else {"kind": r.dp_kind, "ranks": world}}
+        allinfo = [None] * world
+        dist.all_gather_object(allinfo, info)
+        dp_check = {"replicas_identical": all(x["checksum"] == allinfo[0]["checksum"] for x in allinfo),
+                    "per_rank_ms_per_step": [x["ms_per_step"] for x in allinfo],
+                    "communicator": allinfo[0]["dp"],
+                    "peers_per_rank": [x["dp"].get("peers") for x in allinfo]}
     # second figure: rollout only (actors + Gumbel + MPE physics + replay
     # append) over the same env copies, no training
     ro_steps = max(10, args.steps)
@@ -381,6 +433,7 @@ def main():
             "rollout_only_env_steps_per_sec": round(rollout_only, 3),
             "update_rounds": rounds,
             "dp": r.dp_kind if world > 1 else None,
+            "dp_check": dp_check,
             "kernel_pass": {"steps": prof_steps, "event_pair_overhead_ms": round(ev_ms, 5),
                             "per_kind_ms_per_launch": {k: round(v[0] / v[1] - ev_ms, 5) for k, v in per_kind.items()
                                                        if v[1]},
@@ -388,6 +441,8 @@ def main():
             "roofline": roof,
             "throughput_mode": tp_fig,
         }
+        if world == 1 and not args.no_configs2 and args.num_envs != 4096:
+            out["configs2_per_gpu"] = configs2_per_gpu(args)
         if world == 1 and not args.no_gather_stage:
             out["gather_stage"] = gather_stage(r.spec.obs_dims)
         if world == 1 and not args.no_cpu_baseline:
@@ -395,6 +450,12 @@ def main():
             # also the host's cores (the box's CPU share, at most 16)
             out["cpu_baseline"]["all_cores"] = cpu_baseline(args, threads=min(16, os.cpu_count() or 1),
                                                             seconds=max(5.0, args.cpu_seconds / 2))
+            # BASELINE configs[0], the designated CPU config: scenario simple (1 agent), 1 env,
+            # batch 1024, 64-unit MLPs -- 1 pinned core and the host's cores
+            simple = cpu_baseline(args, seconds=max(5.0, args.cpu_seconds / 2), scenario="simple")
+            simple["all_cores"] = cpu_baseline(args, threads=min(16, os.cpu_count() or 1),
+                                               seconds=max(5.0, args.cpu_seconds / 3), scenario="simple")
+            out["cpu_baseline"]["configs0_simple"] = simple
         print(json.dumps(out))
     if world > 1:
         dist.barrier()

@@ -69,6 +69,59 @@ def parse_args(argv=None):
     return parser.parse_args(argv)
 
 
+class LearningCurve:
+    """The reference's episode bookkeeping (train.py:123-133, 164-189) for E env
+    copies that terminate together.
+
+    ``len(episode_rewards)`` is finished episodes + 1 (a fresh 0 entry is
+    appended at every reset).  The reference, whose episodes end one at a
+    time, checks ``len % save_rate == 0`` after each reset and stops once the
+    length exceeds ``num_episodes``; E simultaneous terminations step the
+    length by E, so every multiple of ``save_rate`` crossed -- up to the
+    length the reference stops at, num_episodes + 1 -- gives one print and one
+    curve point, each the mean of the last ``save_rate`` entries at that length
+    (save_rate - 1 finished episodes, in env order, plus the fresh 0).
+    ``read(first, count)`` returns finished episodes [first, first + count) as
+    [count, 1 + n] rows (total, per agent).
+    """
+
+    def __init__(self, save_rate, num_episodes, n):
+        self.save_rate, self.num_episodes, self.n = save_rate, num_episodes, n
+        self.finished = 0
+        self.final_ep_rewards, self.final_ep_ag_rewards = [], []
+
+    @property
+    def length(self):
+        return self.finished + 1
+
+    @property
+    def done(self):
+        return self.length > self.num_episodes
+
+    def finish(self, count, read):
+        """`count` episodes ended; returns [(length, mean reward, per-agent means)]
+        for every save_rate multiple crossed (read=None: count only, no points)."""
+        before = self.length
+        self.finished += count
+        last = min(self.length, self.num_episodes + 1)
+        sr = self.save_rate
+        marks = list(range((before // sr + 1) * sr, last + 1, sr))
+        if not marks or read is None:
+            return []
+        lo = marks[0] - sr                       # first finished episode any window needs
+        span = marks[-1] - 1 - lo
+        log = read(lo, span) if span > 0 else np.zeros((0, 1 + self.n), np.float32)
+        out = []
+        for mk in marks:
+            w = log[mk - sr - lo: mk - 1 - lo]   # episodes [mk - sr, mk - 1) + the fresh 0
+            mean_ep = float(np.sum(w[:, 0], dtype=np.float64) / sr)
+            mean_ag = [float(np.sum(w[:, 1 + j], dtype=np.float64) / sr) for j in range(self.n)]
+            self.final_ep_rewards.append(mean_ep)
+            self.final_ep_ag_rewards.extend(mean_ag)
+            out.append((mk, mean_ep, mean_ag))
+        return out
+
+
 def benchmark(arglist, runner, exp_name, rank):
     """--benchmark (train.py:139-148): run the loaded policies, record every
     agent's scenario benchmark_data() each step, no training.  The reference
@@ -128,7 +181,9 @@ def train(arglist):
                        adv_policy=arglist.adv_policy, batch_size=arglist.batch_size,
                        num_units=arglist.num_units, lr=arglist.lr, gamma=arglist.gamma,
                        max_episode_len=arglist.max_episode_len, seed=arglist.seed,
-                       train_every=arglist.train_every, world_size=world, rank=rank)
+                       train_every=arglist.train_every, world_size=world, rank=rank,
+                       # the learning-curve windows of one terminal step span <= save_rate + E episodes
+                       episode_log_rows=max(4096, 4 * arglist.num_envs, arglist.save_rate + 2 * arglist.num_envs))
     if arglist.update_mode != "strict":
         runner.eng.set_update_mode(arglist.update_mode)
     n = runner.n
@@ -145,10 +200,9 @@ def train(arglist):
         return benchmark(arglist, runner, exp_name, rank)
 
     E, L = arglist.num_envs, arglist.max_episode_len
-    final_ep_rewards, final_ep_ag_rewards = [], []
+    curve = LearningCurve(arglist.save_rate, arglist.num_episodes, n)
     t_start = time.time()
     vec_steps = 0
-    finished = 0                       # finished episodes on this rank
     say('Starting iterations...')
     while True:
         runner.step()
@@ -156,35 +210,28 @@ def train(arglist):
         if vec_steps % L:
             continue
         # every env copy just terminated (train.py:116,127): E new episodes
-        prev = finished
-        finished += E
-        length_before, length_after = prev + 1, finished + 1   # len(episode_rewards)
-        k = length_after // arglist.save_rate - length_before // arglist.save_rate
-        if k > 0 and rank == 0:
+        steps = vec_steps * E
+        points = curve.finish(E, runner.episode_rewards if rank == 0 else None)
+        if points and rank == 0:
             runner.eng.save_state(arglist.save_dir)
-            # np.mean(episode_rewards[-save_rate:]) with the fresh 0 entry included
-            m = min(arglist.save_rate - 1, finished)
-            log = runner.episode_rewards(finished - m, m) if m > 0 else np.zeros((0, 1 + n), np.float32)
-            mean_ep = float(np.sum(log[:, 0], dtype=np.float64) / arglist.save_rate)
-            mean_ag = [float(np.sum(log[:, 1 + j], dtype=np.float64) / arglist.save_rate) for j in range(n)]
-            steps = vec_steps * E
+        for length, mean_ep, mean_ag in points:
+            if rank != 0:
+                break
             if num_adversaries == 0:
                 print("steps: {}, episodes: {}, mean episode reward: {}, time: {}".format(
-                    steps, length_after, mean_ep, round(time.time() - t_start, 3)), flush=True)
+                    steps, length, mean_ep, round(time.time() - t_start, 3)), flush=True)
             else:
                 print("steps: {}, episodes: {}, mean episode reward: {}, agent episode reward: {}, time: {}".format(
-                    steps, length_after, mean_ep, mean_ag, round(time.time() - t_start, 3)), flush=True)
+                    steps, length, mean_ep, mean_ag, round(time.time() - t_start, 3)), flush=True)
             t_start = time.time()
-            final_ep_rewards.append(mean_ep)
-            final_ep_ag_rewards.extend(mean_ag)
-        if length_after > arglist.num_episodes:
+        if curve.done:
             if rank == 0:
                 os.makedirs(arglist.plots_dir, exist_ok=True)
                 with open(arglist.plots_dir + exp_name + '_rewards.pkl', 'wb') as fp:
-                    pickle.dump(final_ep_rewards, fp)
+                    pickle.dump(curve.final_ep_rewards, fp)
                 with open(arglist.plots_dir + exp_name + '_agrewards.pkl', 'wb') as fp:
-                    pickle.dump(final_ep_ag_rewards, fp)
-            say('...Finished total of {} episodes.'.format(length_after))
+                    pickle.dump(curve.final_ep_ag_rewards, fp)
+            say('...Finished total of {} episodes.'.format(curve.length))
             break
     runner.synchronize()
     return runner

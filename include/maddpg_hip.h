@@ -34,7 +34,8 @@ extern "C" {
 
 #define MDP_MAX_AGENTS 8
 #define MDP_ACT_DIM 5          /* MPE Discrete(dim_p*2+1) action spaces */
-#define MDP_ABI_VERSION 1
+#define MDP_MAX_UNITS 256      /* largest --num-units (train.py:24) */
+#define MDP_ABI_VERSION 2
 
 enum mdp_scenario {
     MDP_SCN_NONE = 0,          /* trainer only (no device env) */
@@ -64,7 +65,7 @@ typedef struct mdp_config {
     int32_t obs_dim[MDP_MAX_AGENTS];  /* obs_shape_n (maddpg.py:113) */
     int32_t local_q[MDP_MAX_AGENTS];  /* local_q_func = ddpg (train.py:67-74) */
     int32_t act_dim;                  /* must be MDP_ACT_DIM */
-    int32_t num_units;                /* --num-units (64 or 128) */
+    int32_t num_units;                /* --num-units, 1..MDP_MAX_UNITS (train.py:24) */
     int32_t batch_size;               /* --batch-size */
     int32_t max_episode_len;          /* --max-episode-len */
     int64_t capacity;                 /* ReplayBuffer(1e6) (maddpg.py:147) */
@@ -79,11 +80,16 @@ typedef struct mdp_config {
     float adam_b1, adam_b2, adam_eps; /* TF1 AdamOptimizer defaults */
     double gamma;                     /* --gamma (TD target in fp64, maddpg.py:186) */
     uint64_t seed;                    /* device Philox key (Gumbel noise, env resets) */
+    int32_t episode_log_rows;         /* finished-episode log ring (0: max(4096, 4 num_envs));
+                                         train.py sizes it save_rate + 2 num_envs */
+    int32_t reserved;
 } mdp_config;
 
 typedef struct mdp_tensor_info {      /* one fully_connected{,_1,_2}/{weights,biases} */
     int64_t offset;                   /* floats from the start of a param-space region */
-    int32_t rows, cols;
+    int32_t rows, cols;               /* the TF variable's shape ([in, num_units] ...) */
+    int32_t dev_rows, dev_cols;       /* its block in the arena: num_units padded to the
+                                         kernel width (64/128/256), extra entries zero */
 } mdp_tensor_info;
 
 typedef struct mdp_handle mdp_handle;
@@ -197,6 +203,18 @@ int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles);
 int mdp_dp_xgmi_probe(mdp_handle* h, int32_t* mismatches);
 int mdp_dp_xgmi_enable(mdp_handle* h);
 int mdp_dp_xgmi_close(mdp_handle* h);
+/* what this rank's data parallelism is wired to: out4 = {kind (0 none, 1 RCCL,
+ * 2 direct xGMI), ranks in the communicator (ncclCommCount / exchange world),
+ * this rank, peers reached (RCCL: ranks - 1; xGMI: peer buffers mapped)} */
+int mdp_dp_info(mdp_handle* h, int32_t out4[4]);
+/* Co-residency plan of the spin-waiting optimizer launch (k_reduce_apply: the
+ * chunk workgroups of a tensor wait for each other's norm partials, the xGMI
+ * exchange for the peers' chunks).  For cfg on a device with `cus` CUs that
+ * hold `per_cu` of its 1024-thread workgroups each, out[2 agent + net] = the
+ * launch's grid when the one-launch step is used (grid <= cus x per_cu), or
+ * -grid when that net falls back to k_reduce + k_apply (no spin).  Returns the
+ * number of nets that fall back, < 0 for an invalid cfg.  Needs no GPU. */
+int mdp_ra_plan(const mdp_config* cfg, int32_t cus, int32_t per_cu, int32_t* out);
 /* phase entry points for data parallelism (grad -> all-reduce -> apply) */
 int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev);
 int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev);

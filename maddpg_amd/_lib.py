@@ -21,6 +21,8 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "maddpg_hip.h")
 MAX_AGENTS = 8
 ACT_DIM = 5
 BENCH_W = 8   # MDP_BENCH_W: floats per agent benchmark_data record
+MAX_UNITS = 256  # MDP_MAX_UNITS: largest --num-units
+ABI_VERSION = 2
 
 SCN = {"none": 0, "simple": 1, "simple_spread": 2, "simple_adversary": 3, "simple_tag": 4}
 WHICH = {"actor": 0, "critic": 1, "tgt_actor": 2, "tgt_critic": 3, "m_actor": 4, "v_actor": 5,
@@ -55,11 +57,14 @@ class MdpConfig(ctypes.Structure):
         ("adam_eps", ctypes.c_float),
         ("gamma", ctypes.c_double),
         ("seed", ctypes.c_uint64),
+        ("episode_log_rows", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
 class MdpTensorInfo(ctypes.Structure):
-    _fields_ = [("offset", ctypes.c_int64), ("rows", ctypes.c_int32), ("cols", ctypes.c_int32)]
+    _fields_ = [("offset", ctypes.c_int64), ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
+                ("dev_rows", ctypes.c_int32), ("dev_cols", ctypes.c_int32)]
 
 
 _P = ctypes.c_void_p
@@ -111,6 +116,8 @@ SIGNATURES = {
     "mdp_dp_xgmi_probe": (ctypes.c_int, [_P, _I32P]),
     "mdp_dp_xgmi_enable": (ctypes.c_int, [_P]),
     "mdp_dp_xgmi_close": (ctypes.c_int, [_P]),
+    "mdp_dp_info": (ctypes.c_int, [_P, _I32P]),
+    "mdp_ra_plan": (ctypes.c_int, [ctypes.POINTER(MdpConfig), _I32, _I32, _I32P]),
     "mdp_critic_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_actor_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_reduce_grad": (ctypes.c_int, [_P, _I32, _I32]),
@@ -154,7 +161,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mdp_abi_version() != 1:
+    if lib.mdp_abi_version() != ABI_VERSION:
         raise ImportError("libmaddpg_hip.so ABI version mismatch")
     _lib = lib
     return lib

@@ -117,6 +117,7 @@ struct Layout {
   EnvDesc env;
   int64_t PT = 0;
   int nwg = 0, slab_c = 0, slab_a = 0, eplog_rows = 0, n_ent = 0;
+  int H_log = 0;  // --num-units (topo.H is the padded device width)
   int64_t off[MDP_R_COUNT];
   int64_t bytes[MDP_R_COUNT];
   int64_t total = 0;
@@ -126,15 +127,21 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   if (!c) { err = "null config"; return false; }
   if (c->n_agents < 1 || c->n_agents > MDP_MAX_AGENTS) { err = "n_agents out of range"; return false; }
   if (c->act_dim != MDP_ACT_DIM) { err = "act_dim must be 5 (MPE Discrete(5))"; return false; }
-  if (c->num_units != 64 && c->num_units != 128) { err = "num_units must be 64 or 128"; return false; }
+  if (c->num_units < 1 || c->num_units > MDP_MAX_UNITS) { err = "num_units must be in [1, 256]"; return false; }
   if (c->batch_size < 1) { err = "batch_size must be >= 1"; return false; }
   if (c->capacity < 1 || c->capacity > (int64_t(1) << 31) - 1) { err = "capacity out of range"; return false; }
   if (c->num_envs < 0) { err = "num_envs < 0"; return false; }
-  const int n = c->n_agents, H = c->num_units;
+  // --num-units is any width (train.py:24); the device nets are H wide with H
+  // the kernel width that holds it.  The extra hidden units have zero weights
+  // and biases: relu(0) = 0 feeds nothing forward, their gradients are exactly
+  // zero (ReLU mask / zero input activations), so Adam and Polyak keep them at
+  // zero and every logical output is bit-identical to an unpadded net.
+  const int n = c->n_agents, H = mdp_device_units(c->num_units);
   Topo& T = L.topo;
   std::memset(&T, 0, sizeof(T));
   T.n = n;
   T.H = H;
+  L.H_log = c->num_units;
   int sum_obs = 0, obs_max = 0;
   for (int i = 0; i < n; ++i) {
     if (c->obs_dim[i] < 1 || c->obs_dim[i] > 256) { err = "obs_dim out of range"; return false; }
@@ -185,7 +192,8 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
     std::memset(&L.env, 0, sizeof(L.env));
   }
   L.n_ent = n + L.env.n_landmarks;
-  L.eplog_rows = std::max(4096, 4 * E);
+  if (c->episode_log_rows < 0) { err = "episode_log_rows < 0"; return false; }
+  L.eplog_rows = c->episode_log_rows > 0 ? c->episode_log_rows : std::max(4096, 4 * E);
   int64_t sz[MDP_R_COUNT];
   sz[MDP_R_THETA] = sz[MDP_R_TARGET] = sz[MDP_R_ADAM_M] = sz[MDP_R_ADAM_V] = sz[MDP_R_GRAD] = 4 * L.PT;
   sz[MDP_R_REPLAY] = 4 * c->capacity * T.row_stride;
@@ -260,6 +268,7 @@ struct mdp_handle {
   Ctl* ctl;
   int64_t len = 0, next = 0;  // host mirror of the ring
   uint32_t act_ctr = 0, reset_ctr = 0;
+  bool env_lockstep = true;   // every env copy at the same episode step (log in env order)
   std::string err;
   bool prof_on[MDP_K_COUNT] = {};
   std::vector<hipEvent_t> ev[MDP_K_COUNT];
@@ -291,12 +300,16 @@ struct mdp_handle {
   FusedApplyArgs* tp_list = nullptr;  // device copy of the 2n optimizer steps (throughput mode)
   RaBatch tp_batch;                   // single GPU: reduce + step
   RaBatch tp_reduce, tp_step;         // data parallel: reduce pass, all-reduce, step pass (x 1/G)
+  // co-residency of the spin-waiting optimizer launches (k_reduce_apply's
+  // norm handshake, the xGMI exchange): CUs x resident workgroups per CU of
+  // k_reduce_apply / k_reduce_apply_batch, measured at create
+  int ra_cap = 0, ra_batch_cap = 0;
+  bool tp_fits[4] = {true, true, true, true};  // per RaBatch: whole grid co-resident
+  std::vector<FusedApplyArgs> tp_host[4];     // the batches' entries, for per-net launches
   RaBatch tp_xchg;                    // data parallel over xGMI: reduce + exchange + step (x 1/G)
   // the xGMI batch only when its whole grid is co-resident (every chunk
   // workgroup spins on its peers' matching chunk); otherwise one launch per net
-  bool tp_xchg_fits = true;
   bool rollout_draw = true;           // step_launches: first-round draw inside k_rollout
-  std::vector<FusedApplyArgs> tp_xchg_host;
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
   uint64_t* xbuf = nullptr;
@@ -395,9 +408,21 @@ const NDesc& net_of(mdp_handle* h, int agent, int net) {
   return net ? h->L.topo.ag[agent].critic : h->L.topo.ag[agent].actor;
 }
 
-int64_t net_floats(const NDesc& d) {
+// logical (TF variable) shape of tensor t of a net whose device width is padded:
+// (W1 [in, u], b1 [u], W2 [u, u], b2 [u], W3 [u, out], b3 [out], u = --num-units)
+void logical_shape(const mdp_handle* h, const NDesc& d, int t, int* rows, int* cols) {
+  const int u = h->L.H_log;
+  *rows = (t == 2 || t == 4) ? u : d.t[t].rows;
+  *cols = t < 4 ? u : d.t[t].cols;
+}
+
+int64_t net_floats(const mdp_handle* h, const NDesc& d) {
   int64_t s = 0;
-  for (int t = 0; t < 6; ++t) s += (int64_t)d.t[t].rows * d.t[t].cols;
+  for (int t = 0; t < 6; ++t) {
+    int r, c;
+    logical_shape(h, d, t, &r, &c);
+    s += (int64_t)r * c;
+  }
   return s;
 }
 
@@ -455,7 +480,7 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   while (G > 1 && lds_critic_bytes(h->L.topo, G) > MDP_LDS_BUDGET) --G;
   if (lds_critic_bytes(h->L.topo, G) > MDP_LDS_BUDGET) return fail(h, "critic step does not fit in LDS");
   a.group = G;
-  HIPCHK(h, mdp_launch_critic_grad(a, h->cfg.num_units, lds_critic_bytes(h->L.topo, G), h->stream));
+  HIPCHK(h, mdp_launch_critic_grad(a, h->L.topo.H, lds_critic_bytes(h->L.topo, G), h->stream));
   return 0;
 }
 
@@ -486,7 +511,7 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
     return 0;
   }
-  HIPCHK(h, mdp_launch_actor_grad(a, h->cfg.num_units, lds_actor_bytes(h->L.topo), h->stream));
+  HIPCHK(h, mdp_launch_actor_grad(a, h->L.topo.H, lds_actor_bytes(h->L.topo), h->stream));
   return 0;
 }
 
@@ -543,12 +568,13 @@ int do_apply(mdp_handle* h, int agent, int net, bool from_slab, float scale) {
 }
 
 // batch reduction + clip + Adam (+ Polyak, stats, beta advance) in one launch
-// (single GPU); false when a tensor has more chunks than the sync area holds
+// (single GPU, and the xGMI exchange).  Its chunk workgroups spin on each other
+// (the per-tensor norm handshake; the exchange also on the peers' matching
+// chunk), so the launch is used only when its whole grid is co-resident --
+// grid <= CUs x resident workgroups per CU -- and every tensor's chunks fit the
+// sync area; otherwise the step runs as k_reduce + k_apply (no spin).
 bool reduce_apply_ok(const mdp_handle* h, int agent, int net) {
-  const NDesc& d = net ? h->L.topo.ag[agent].critic : h->L.topo.ag[agent].actor;
-  for (int t = 0; t < 6; ++t)
-    if ((d.t[t].rows * d.t[t].cols + MDP_RA_CHUNK - 1) / MDP_RA_CHUNK > MDP_RA_MAXCH) return false;
-  return true;
+  return mdp_ra_fits(h->L.topo, agent, net, h->ra_cap);
 }
 
 FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net) {
@@ -628,6 +654,7 @@ struct RcclApi {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) err = nullptr;
+  decltype(&ncclCommCount) count = nullptr;
 };
 RcclApi& rccl() {
   static RcclApi r;
@@ -641,6 +668,7 @@ RcclApi& rccl() {
       r.all_reduce = (decltype(r.all_reduce))dlsym(so, "ncclAllReduce");
       r.destroy = (decltype(r.destroy))dlsym(so, "ncclCommDestroy");
       r.err = (decltype(r.err))dlsym(so, "ncclGetErrorString");
+      r.count = (decltype(r.count))dlsym(so, "ncclCommCount");
       r.ok = r.get_id && r.init_rank && r.all_reduce && r.destroy && r.err;
     }
   }
@@ -778,13 +806,10 @@ int tp_setup(mdp_handle* h) {
         rb.wg_start[q + 1] = rb.wg_start[q] + mdp_ra_grid(f);
       }
   }
-  h->tp_xchg_host.assign(list.begin() + 6 * n, list.end());
-  {
-    int dev = 0, cus = 0, per_cu = 0;
-    HIPCHK(h, hipGetDevice(&dev));
-    HIPCHK(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    HIPCHK(h, mdp_ra_batch_occupancy(&per_cu));
-    h->tp_xchg_fits = (int64_t)h->tp_xchg.wg_start[2 * n] <= (int64_t)cus * per_cu;
+  for (int ph = 0; ph < 4; ++ph) {
+    h->tp_host[ph].assign(list.begin() + 2 * n * ph, list.begin() + 2 * n * (ph + 1));
+    // phase 1 (reduce only) never spins; the others need the whole batch co-resident
+    h->tp_fits[ph] = ph == 1 || rbs[ph]->wg_start[2 * n] <= h->ra_batch_cap;
   }
   HIPCHK(h, hipMalloc((void**)&h->tp_list, sizeof(FusedApplyArgs) * list.size()));
   HIPCHK(h, hipMemcpy(h->tp_list, list.data(), sizeof(FusedApplyArgs) * list.size(), hipMemcpyHostToDevice));
@@ -869,33 +894,40 @@ int tp_grads_general(mdp_handle* h, const int32_t* idx, const float* u_tgt, cons
   return 0;
 }
 
+// the optimizer steps of every net in one launch when the batch grid is
+// co-resident (its chunk workgroups spin), else one launch per net (e.g. tag
+// N=6 at H=128: ~1,350 chunk workgroups; each net's own grid fits)
+int launch_tp_batch(mdp_handle* h, int ph) {
+  const RaBatch* rbs[4] = {&h->tp_batch, &h->tp_reduce, &h->tp_step, &h->tp_xchg};
+  if (h->tp_fits[ph]) {
+    HIPCHK(h, mdp_launch_reduce_apply_batch(*rbs[ph], h->stream));
+    return 0;
+  }
+  for (const FusedApplyArgs& f : h->tp_host[ph]) HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
+  return 0;
+}
+
 int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
   const int rc = tp_fast(h) ? tp_grads_fast(h, idx, u_tgt, u_act, pf_out)
                             : tp_grads_general(h, idx, u_tgt, u_act, pf_out);
   if (rc) return rc;
   if (h->p2p) {  // data parallel over xGMI: reduce + exchange + step of every net, one launch
     ProfScope p(h, MDP_K_REDUCE_APPLY);
-    if (h->tp_xchg_fits) {
-      HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_xchg, h->stream));
-    } else {  // e.g. tag N=6 at H=128: ~1,350 chunk workgroups, one launch per net instead
-      for (const FusedApplyArgs& f : h->tp_xchg_host) HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
-    }
-    return 0;
+    return launch_tp_batch(h, 3);
   }
   if (h->comm) {  // data parallel: ONE all-reduce of every net's gradient per round
     {
       ProfScope p(h, MDP_K_REDUCE);
-      HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_reduce, h->stream));
+      const int rc = launch_tp_batch(h, 1);
+      if (rc) return rc;
     }
     const int rc = dp_allreduce_all(h);
     if (rc) return rc;
     ProfScope p(h, MDP_K_APPLY);
-    HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_step, h->stream));
-    return 0;
+    return launch_tp_batch(h, 2);
   }
   ProfScope p(h, MDP_K_REDUCE_APPLY);
-  HIPCHK(h, mdp_launch_reduce_apply_batch(h->tp_batch, h->stream));
-  return 0;
+  return launch_tp_batch(h, 0);
 }
 
 int set_ring(mdp_handle* h, int64_t len, int64_t next) {
@@ -918,6 +950,21 @@ int64_t mdp_arena_bytes(const mdp_config* cfg, int64_t* param_floats) {
   if (!build_layout(cfg, L, err)) return -1;
   if (param_floats) *param_floats = L.PT;
   return L.total;
+}
+
+int mdp_ra_plan(const mdp_config* cfg, int32_t cus, int32_t per_cu, int32_t* out) {
+  Layout L;
+  std::string err;
+  if (!build_layout(cfg, L, err) || cus < 0 || per_cu < 0) return -1;
+  int fallback = 0;
+  for (int i = 0; i < cfg->n_agents; ++i)
+    for (int net = 0; net < 2; ++net) {
+      const int g = mdp_ra_grid_of(L.topo, i, net);
+      const bool ok = mdp_ra_fits(L.topo, i, net, cus * per_cu);
+      if (out) out[2 * i + net] = ok ? g : -g;
+      fallback += ok ? 0 : 1;
+    }
+  return fallback;
 }
 
 int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void* hip_stream, mdp_handle** out) {
@@ -946,6 +993,14 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
   }
   *out = h;
   HIPCHK(h, hipGetDevice(&h->device));
+  {
+    int cus = 0, per = 0, per_b = 0;
+    HIPCHK(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+    HIPCHK(h, mdp_ra_occupancy(&per));
+    HIPCHK(h, mdp_ra_batch_occupancy(&per_b));
+    h->ra_cap = cus * per;
+    h->ra_batch_cap = cus * per_b;
+  }
   if (hip_stream) {
     h->stream = (hipStream_t)hip_stream;
   } else {
@@ -1053,8 +1108,9 @@ int mdp_tensor(const mdp_handle* h, int32_t agent, int32_t net, int32_t t, mdp_t
   if (!h || agent < 0 || agent >= h->cfg.n_agents || t < 0 || t > 5 || !out) return -1;
   const NDesc& d = net ? h->L.topo.ag[agent].critic : h->L.topo.ag[agent].actor;
   out->offset = d.t[t].off;
-  out->rows = d.t[t].rows;
-  out->cols = d.t[t].cols;
+  logical_shape(h, d, t, &out->rows, &out->cols);
+  out->dev_rows = d.t[t].rows;
+  out->dev_cols = d.t[t].cols;
   return 0;
 }
 
@@ -1075,13 +1131,14 @@ int mdp_set_params(mdp_handle* h, int32_t agent, int32_t which, const float* src
   int region, net;
   if (region_for(which, &region, &net)) return fail(h, "bad param set id");
   const NDesc& d = net_of(h, agent, net);
-  if (n != net_floats(d)) return fail(h, "param count mismatch");
-  std::vector<float> buf(d.size, 0.f);
+  if (n != net_floats(h, d)) return fail(h, "param count mismatch");
+  std::vector<float> buf(d.size, 0.f);  // padded entries stay zero
   int64_t s = 0;
   for (int t = 0; t < 6; ++t) {
-    const int64_t k = (int64_t)d.t[t].rows * d.t[t].cols;
-    std::memcpy(buf.data() + (d.t[t].off - d.off), src + s, 4 * k);
-    s += k;
+    int rows, cols;
+    logical_shape(h, d, t, &rows, &cols);
+    for (int r = 0; r < rows; ++r, s += cols)
+      std::memcpy(buf.data() + (d.t[t].off - d.off) + (int64_t)r * d.t[t].cols, src + s, 4 * (int64_t)cols);
   }
   float* dst = (float*)(h->arena + h->L.off[region]) + d.off;
   HIPCHK(h, hipMemcpyAsync(dst, buf.data(), 4 * buf.size(), hipMemcpyHostToDevice, h->stream));
@@ -1094,16 +1151,17 @@ int mdp_get_params(mdp_handle* h, int32_t agent, int32_t which, float* dst, int6
   int region, net;
   if (region_for(which, &region, &net)) return fail(h, "bad param set id");
   const NDesc& d = net_of(h, agent, net);
-  if (n != net_floats(d)) return fail(h, "param count mismatch");
+  if (n != net_floats(h, d)) return fail(h, "param count mismatch");
   std::vector<float> buf(d.size);
   const float* src = (const float*)(h->arena + h->L.off[region]) + d.off;
   HIPCHK(h, hipMemcpyAsync(buf.data(), src, 4 * buf.size(), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int64_t s = 0;
   for (int t = 0; t < 6; ++t) {
-    const int64_t k = (int64_t)d.t[t].rows * d.t[t].cols;
-    std::memcpy(dst + s, buf.data() + (d.t[t].off - d.off), 4 * k);
-    s += k;
+    int rows, cols;
+    logical_shape(h, d, t, &rows, &cols);
+    for (int r = 0; r < rows; ++r, s += cols)
+      std::memcpy(dst + s, buf.data() + (d.t[t].off - d.off) + (int64_t)r * d.t[t].cols, 4 * (int64_t)cols);
   }
   return 0;
 }
@@ -1206,7 +1264,7 @@ int mdp_act(mdp_handle* h, int32_t agent, int32_t target, const float* obs_dev, 
   a.seed = h->cfg.seed;
   a.stream = 0x40000u | (uint32_t)(agent << 1) | (uint32_t)(target ? 1 : 0);
   a.ctr = h->act_ctr++;
-  HIPCHK(h, mdp_launch_eval(a, h->cfg.num_units, lds_eval_bytes(a.in, h->cfg.num_units), h->stream));
+  HIPCHK(h, mdp_launch_eval(a, h->L.topo.H, lds_eval_bytes(a.in, h->L.topo.H), h->stream));
   return 0;
 }
 
@@ -1227,7 +1285,7 @@ int mdp_actor_logits(mdp_handle* h, int32_t agent, int32_t target, const float* 
   a.seed = h->cfg.seed;
   a.stream = 0;
   a.ctr = 0;
-  HIPCHK(h, mdp_launch_eval(a, h->cfg.num_units, lds_eval_bytes(a.in, h->cfg.num_units), h->stream));
+  HIPCHK(h, mdp_launch_eval(a, h->L.topo.H, lds_eval_bytes(a.in, h->L.topo.H), h->stream));
   return 0;
 }
 
@@ -1247,7 +1305,7 @@ int mdp_q_values(mdp_handle* h, int32_t agent, int32_t target, const float* x_de
   a.seed = h->cfg.seed;
   a.stream = 0;
   a.ctr = 0;
-  HIPCHK(h, mdp_launch_eval(a, h->cfg.num_units, lds_eval_bytes(a.in, h->cfg.num_units), h->stream));
+  HIPCHK(h, mdp_launch_eval(a, h->L.topo.H, lds_eval_bytes(a.in, h->L.topo.H), h->stream));
   return 0;
 }
 
@@ -1464,6 +1522,25 @@ int mdp_dp_xgmi_close(mdp_handle* h) {
   return 0;
 }
 
+int mdp_dp_info(mdp_handle* h, int32_t out4[4]) {
+  if (!h || !out4) return -1;
+  out4[0] = h->p2p ? 2 : (h->comm ? 1 : 0);
+  out4[1] = 1;
+  out4[2] = h->cfg.rank;
+  out4[3] = 0;
+  if (h->p2p) {
+    out4[1] = h->x_world;
+    out4[2] = h->x_rank;
+    for (void* p : h->x_opened) out4[3] += p ? 1 : 0;
+  } else if (h->comm) {
+    int c = h->dp_world;
+    if (rccl().count && rccl().count(h->comm, &c) != ncclSuccess) return fail(h, "ncclCommCount failed");
+    out4[1] = c;
+    out4[3] = c - 1;
+  }
+  return 0;
+}
+
 int mdp_set_graphs(mdp_handle* h, int32_t on) {
   h->graphs = on != 0;
   return 0;
@@ -1564,6 +1641,7 @@ int mdp_env_reset(mdp_handle* h) {
   a.ep_step = h->ep_step;
   a.ep_rew = h->ep_rew;
   HIPCHK(h, mdp_launch_env_reset(a, h->stream));
+  h->env_lockstep = true;
   return 0;
 }
 
@@ -1586,6 +1664,7 @@ static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* 
   a.ep_rew = h->ep_rew;
   a.eplog = h->eplog;
   a.eplog_cap = h->L.eplog_rows;
+  a.eplog_by_env = h->env_lockstep ? 1 : 0;
   a.ctl = h->ctl;
   a.seed = h->cfg.seed;
   a.E = h->cfg.num_envs;
@@ -1595,7 +1674,7 @@ static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* 
   a.ticket = &h->ctl->ticket[2];
   a.bench = bench;
   ProfScope p(h, MDP_K_ROLLOUT);
-  HIPCHK(h, mdp_launch_rollout(a, h->cfg.num_units, lds_rollout_bytes(h->L.topo), h->stream));
+  HIPCHK(h, mdp_launch_rollout(a, h->L.topo.H, lds_rollout_bytes(h->L.topo), h->stream));
   return 0;
 }
 
@@ -1645,41 +1724,51 @@ static int step_launches(mdp_handle* h, int rounds) {
   return rc;
 }
 
-int mdp_train_step(mdp_handle* h, int32_t rounds) {
-  if (need_env(h)) return -1;
-  if (rounds < 0 || rounds > 64) return fail(h, "mdp_train_step: rounds must be in [0, 64]");
-  if (rounds > 0 && h->len + h->cfg.num_envs <= 0) return fail(h, "update round on an empty replay buffer");
-  int rc = 0;
-  // the index kernels read the ring length the rollout leaves (device Ctl); the
-  // host mirror moves first so the empty-buffer guard sees the same state
-  advance_ring_mirror(h);
+// the launches of one training step (eager, or captured once per round count and replayed)
+static int train_step_body(mdp_handle* h, int rounds) {
   // RCCL collectives are launched eagerly unless asked; the xGMI exchange is
   // inside the optimizer kernels, so those steps are always captured
   const bool no_graph = h->comm && !h->dp_graphs;
   if (!h->graphs || no_graph || any_prof(h) || h->eager_steps < 1 || rounds == 0) {
     if (rounds > 0) ++h->eager_steps;  // first training step eager (one-time kernel attribute setup)
-    rc = step_launches(h, rounds);
-  } else {
-    auto it = h->step_exec.find(rounds);
-    if (it == h->step_exec.end()) {
-      HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-      h->capturing = true;
-      rc = step_launches(h, rounds);
-      h->capturing = false;
-      hipGraph_t g = nullptr;
-      const hipError_t e = hipStreamEndCapture(h->stream, &g);
-      if (rc) {
-        if (g) (void)hipGraphDestroy(g);
-        return rc;
-      }
-      if (e != hipSuccess) return fail(h, "hipStreamEndCapture", e);
-      hipGraphExec_t x = nullptr;
-      const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(g);
-      if (ei != hipSuccess) return fail(h, "hipGraphInstantiate", ei);
-      it = h->step_exec.emplace(rounds, x).first;
+    return step_launches(h, rounds);
+  }
+  auto it = h->step_exec.find(rounds);
+  if (it == h->step_exec.end()) {
+    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    h->capturing = true;
+    const int rc = step_launches(h, rounds);
+    h->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
     }
-    HIPCHK(h, hipGraphLaunch(it->second, h->stream));
+    if (e != hipSuccess) return fail(h, "hipStreamEndCapture", e);
+    hipGraphExec_t x = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) return fail(h, "hipGraphInstantiate", ei);
+    it = h->step_exec.emplace(rounds, x).first;
+  }
+  HIPCHK(h, hipGraphLaunch(it->second, h->stream));
+  return 0;
+}
+
+int mdp_train_step(mdp_handle* h, int32_t rounds) {
+  if (need_env(h)) return -1;
+  if (rounds < 0 || rounds > 64) return fail(h, "mdp_train_step: rounds must be in [0, 64]");
+  if (rounds > 0 && h->len + h->cfg.num_envs <= 0) return fail(h, "update round on an empty replay buffer");
+  // the index kernels read the ring length the rollout leaves (device Ctl); the
+  // host mirror moves first so the empty-buffer guard sees the same state, and
+  // moves back when the step could not be launched
+  const int64_t len0 = h->len, next0 = h->next;
+  advance_ring_mirror(h);
+  const int rc = train_step_body(h, rounds);
+  if (rc) {
+    h->len = len0;
+    h->next = next0;
   }
   return rc;
 }
@@ -1701,7 +1790,10 @@ int mdp_env_set_state(mdp_handle* h, const float* pos, const float* vel, const i
   if (pos) HIPCHK(h, hipMemcpyAsync(h->pos, pos, 4 * E * ne * 2, hipMemcpyHostToDevice, h->stream));
   if (vel) HIPCHK(h, hipMemcpyAsync(h->vel, vel, 4 * E * ne * 2, hipMemcpyHostToDevice, h->stream));
   if (goal) HIPCHK(h, hipMemcpyAsync(h->goal, goal, 4 * E, hipMemcpyHostToDevice, h->stream));
-  if (ep_step) HIPCHK(h, hipMemcpyAsync(h->ep_step, ep_step, 4 * E, hipMemcpyHostToDevice, h->stream));
+  if (ep_step) {
+    HIPCHK(h, hipMemcpyAsync(h->ep_step, ep_step, 4 * E, hipMemcpyHostToDevice, h->stream));
+    h->env_lockstep = std::all_of(ep_step, ep_step + E, [&](int32_t s) { return s == ep_step[0]; });
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return 0;
 }

@@ -15,8 +15,11 @@
 // every chunk derives the identical norm.  The epoch (sync counter 7 of the
 // net) is read at the start and advanced by the last workgroup, so the slots
 // never need a reset and a stale pair never carries the awaited tag.
-// The grid (<= a few dozen workgroups) is always co-resident; every spin is
-// bounded and records a fault in Ctl instead of hanging.
+// The host launches it only when the whole grid is co-resident (grid <= CUs x
+// resident workgroups per CU, mdp_ra_fits; otherwise k_reduce + k_apply);
+// every spin is bounded and records a fault in Ctl instead of hanging, and
+// once a fault is recorded no launch writes the optimizer state any more (a
+// faulted step leaves m, v, theta, targets and the beta powers untouched).
 //
 // Then TF1 ApplyAdam on the chunk (+ Polyak of the chunk for the actor step),
 // Polyak workgroups of the other net, the stats workgroup -- exactly as k_apply
@@ -255,7 +258,10 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
         }
         tot = wave_sum_d(tot);
       }
-      if (act) {
+      // a timed-out handshake or exchange (this launch or an earlier one)
+      // leaves the optimizer state as it was
+      const bool faulted = __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      if (act && !faulted) {
         const float norm = (float)sqrt(tot);
         const float clip = a.clip;
         const float denom = fmaxf(norm, clip);
@@ -279,6 +285,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       }  // phase != 1
     }
   } else if (a.polyak && b < f.rblk[6] + a.oblk[6]) {
+    if (__hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     const int bb = b - f.rblk[6];
     int t = 0;
     while (bb >= a.oblk[t + 1]) ++t;
@@ -355,11 +362,13 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
   if (tid == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(f.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev % nb == nb - 1) {
-      const float p1 = a.beta[0], p2 = a.beta[1];
-      a.beta[2] = p1;
-      a.beta[3] = p2;
-      a.beta[0] = p1 * a.b1;
-      a.beta[1] = p2 * a.b2;
+      if (__hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        const float p1 = a.beta[0], p2 = a.beta[1];
+        a.beta[2] = p1;
+        a.beta[3] = p2;
+        a.beta[0] = p1 * a.b1;
+        a.beta[1] = p2 * a.b2;
+      }
       if (a.bump_ctr) a.ctl->upd_ctr += (uint32_t)a.bump_ctr;
       if (f.phase == 3) f.xstep[0] += 1u;
       f.sync_ctr[7 * 32] += 1u;
@@ -388,6 +397,11 @@ int mdp_ra_grid(const FusedApplyArgs& f) {
 hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce_apply, dim3(mdp_ra_grid(f)), dim3(1024), 0, s, f);
   return hipGetLastError();
+}
+
+// co-resident k_reduce_apply workgroups per CU
+hipError_t mdp_ra_occupancy(int* per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_reduce_apply, 1024, 0);
 }
 
 // co-resident k_reduce_apply_batch workgroups per CU

@@ -249,6 +249,31 @@ __device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const 
                                           const float* __restrict__ b, int nout, float* out, int ldo) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int c = min(r, nout - 1), kmax = K - 1;
+  if constexpr (KS > 32) {
+    // wide heads (H = 256): 64-deep chunks, one round trip each, so the
+    // fragments fit the register budget of a 1024-thread workgroup.  Same
+    // accumulator and k order as the one-shot form.
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < K; c0 += 4 * MDP_KC) {
+      float w[MDP_KC], x[MDP_KC];
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s) {
+        const int k = c0 + 4 * s + kq;
+        const float v = W[min(k, kmax) * nout + c];
+        w[s] = (r < nout && k < K) ? v : 0.f;
+        x[s] = X[r * ldx + min(k, kmax)];
+      }
+#pragma unroll
+      for (int s = 0; s < MDP_KC; ++s)
+        if (c0 + 4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+    }
+    const float bias = b[c];
+    if (r < nout) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[(kq * 4 + i) * ldo + r] = acc[i] + bias;
+    }
+    return;
+  }
   float w[KS], x[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {

@@ -312,7 +312,7 @@ __device__ __forceinline__ void wgrad_tile(const float* X, int ldx, int K, const
 }
 }  // namespace
 
-static_assert(MDP_GEN_THREADS / 64 >= 128 / 16, "one single-net layer tile per wave (pf_load / *_pf)");
+static_assert(MDP_GEN_THREADS / 64 >= MDP_MAX_UNITS / 16, "one single-net layer tile per wave (pf_load / *_pf)");
 
 template <int H>
 __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
@@ -783,10 +783,20 @@ hipError_t launch_actor(const ActorArgs& a, int lds, hipStream_t s) {
 }  // namespace
 
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s) {
-  return H == 64 ? launch_critic<64>(a, lds_bytes, s) : launch_critic<128>(a, lds_bytes, s);
+  switch (H) {
+    case 64: return launch_critic<64>(a, lds_bytes, s);
+    case 128: return launch_critic<128>(a, lds_bytes, s);
+    case 256: return launch_critic<256>(a, lds_bytes, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s) {
-  return H == 64 ? launch_actor<64>(a, lds_bytes, s) : launch_actor<128>(a, lds_bytes, s);
+  switch (H) {
+    case 64: return launch_actor<64>(a, lds_bytes, s);
+    case 128: return launch_actor<128>(a, lds_bytes, s);
+    case 256: return launch_actor<256>(a, lds_bytes, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 #ifdef MDP_STAMPS

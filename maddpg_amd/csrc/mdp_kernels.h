@@ -147,6 +147,10 @@ struct RolloutArgs {
   float* ep_rew;
   float* eplog;
   int64_t eplog_cap;
+  // env copies in lockstep (all terminate on the same step): episode e of a
+  // step is logged at slot episodes + e -- env order, deterministic; otherwise
+  // in arrival order
+  int eplog_by_env;
   Ctl* ctl;
   uint64_t seed;
   int E, env_base;
@@ -193,6 +197,10 @@ struct EvalArgs {
   uint64_t seed;
   uint32_t stream, ctr;
 };
+
+// kernel width that serves --num-units u: the gradient / rollout / eval kernels
+// are instantiated for H = 64, 128, 256 (the fast register-resident ones for 64)
+inline int mdp_device_units(int u) { return u <= 64 ? 64 : (u <= 128 ? 128 : 256); }
 
 // ---- dynamic LDS sizes (must mirror the LdsCarve order in the kernels)
 inline int mdp_r4(int n) { return (n + 3) & ~3; }
@@ -258,6 +266,28 @@ struct RaBatch {
   int wg_start[MDP_RA_BATCH_MAX + 1];
 };
 int mdp_ra_grid(const FusedApplyArgs& f);
+hipError_t mdp_ra_occupancy(int* per_cu);   // co-resident k_reduce_apply workgroups per CU
+// grid of the fused optimizer launch of (agent, net): the 256-parameter chunks
+// of the net, for the actor step the Polyak workgroups of the critic, one stats
+// workgroup (mirrors fused_args_for / apply_args / mdp_ra_grid)
+inline int mdp_ra_grid_of(const Topo& t, int agent, int net) {
+  const NDesc& d = net ? t.ag[agent].critic : t.ag[agent].actor;
+  const NDesc& o = net ? t.ag[agent].actor : t.ag[agent].critic;
+  int g = 1;
+  for (int k = 0; k < 6; ++k) {
+    g += (d.t[k].rows * d.t[k].cols + MDP_RA_CHUNK - 1) / MDP_RA_CHUNK;
+    if (!net) g += (o.t[k].rows * o.t[k].cols + MDP_APPLY_CHUNK - 1) / MDP_APPLY_CHUNK;
+  }
+  return g;
+}
+// the fused launch is safe: every tensor's chunks fit the sync area and the
+// whole grid is co-resident on `capacity` workgroup slots
+inline bool mdp_ra_fits(const Topo& t, int agent, int net, int capacity) {
+  const NDesc& d = net ? t.ag[agent].critic : t.ag[agent].actor;
+  for (int k = 0; k < 6; ++k)
+    if ((d.t[k].rows * d.t[k].cols + MDP_RA_CHUNK - 1) / MDP_RA_CHUNK > MDP_RA_MAXCH) return false;
+  return mdp_ra_grid_of(t, agent, net) <= capacity;
+}
 hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s);
 hipError_t mdp_ra_batch_occupancy(int* per_cu);
 // connection probe of the xGMI exchange: nchunk chunks of a rank-tagged

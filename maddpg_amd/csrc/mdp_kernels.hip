@@ -683,6 +683,7 @@ __device__ __forceinline__ void rollout_finish(const RolloutArgs& a, int64_t nex
     a.ctl->next = (next + a.E) % a.cap;
     a.ctl->len = len + a.E < a.cap ? len + a.E : a.cap;
     a.ctl->env_steps += 1;
+    a.ctl->episodes += atomicExch(&a.ctl->ep_pending, 0u);
     *a.ticket = 0u;
   }
 }
@@ -707,6 +708,7 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   const int nvalid = min(MDP_R, a.E - e0);
   const int64_t next = a.ctl->next, len = a.ctl->len;
   const uint32_t step = (uint32_t)a.ctl->env_steps;
+  const int64_t ep_base = a.ctl->episodes;  // advanced only by this launch's last workgroup
   if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
     // the index draw of the step's first round, off the critical path: the
     // MT state is untouched by the env workgroups, and the length is the one
@@ -786,8 +788,9 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     }
     const int st = a.ep_step[e] + 1;
     if (st >= E.max_ep_len) {  // terminal -> log episode, env.reset() (train.py:127-133)
-      const unsigned long long slot = atomicAdd((unsigned long long*)&a.ctl->episodes, 1ull);
-      float* lgp = a.eplog + (int64_t)(slot % (unsigned long long)a.eplog_cap) * (1 + n);
+      const uint32_t q = atomicAdd(&a.ctl->ep_pending, 1u);
+      const int64_t slot = ep_base + (a.eplog_by_env ? (int64_t)e : (int64_t)q);
+      float* lgp = a.eplog + (slot % a.eplog_cap) * (1 + n);
       lgp[0] = tot;
       for (int j = 0; j < n; ++j) {
         lgp[1 + j] = a.ep_rew[(int64_t)e * n + j];
@@ -886,6 +889,7 @@ static void ensure_lds_limits() {
   if (!set_lds_limit_done) {
     raise_lds_limits<64>();
     raise_lds_limits<128>();
+    raise_lds_limits<256>();
     (void)hipGetLastError();  // an unsupported opt-in must not poison the next launch check
     set_lds_limit_done = 1;
   }
@@ -893,11 +897,21 @@ static void ensure_lds_limits() {
 
 hipError_t mdp_launch_rollout(const RolloutArgs& a, int H, int lds_bytes, hipStream_t s) {
   ensure_lds_limits();
-  return H == 64 ? launch_rollout_t<64>(a, lds_bytes, s) : launch_rollout_t<128>(a, lds_bytes, s);
+  switch (H) {
+    case 64: return launch_rollout_t<64>(a, lds_bytes, s);
+    case 128: return launch_rollout_t<128>(a, lds_bytes, s);
+    case 256: return launch_rollout_t<256>(a, lds_bytes, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t s) {
   ensure_lds_limits();
-  return H == 64 ? launch_eval_t<64>(a, lds_bytes, s) : launch_eval_t<128>(a, lds_bytes, s);
+  switch (H) {
+    case 64: return launch_eval_t<64>(a, lds_bytes, s);
+    case 128: return launch_eval_t<128>(a, lds_bytes, s);
+    case 256: return launch_eval_t<256>(a, lds_bytes, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s) {
   const int grid = a.blk[6] + (a.polyak ? a.oblk[6] : 0) + (a.stats_mode ? 1 : 0);

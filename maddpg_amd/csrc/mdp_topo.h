@@ -60,4 +60,6 @@ struct Ctl {
   uint32_t upd_ctr;     // RNG counter for training noise
   uint32_t fault;       // set by a bounded spin that timed out (1 norm handshake, 2 xGMI exchange)
   uint32_t xstep[16];   // xGMI exchanges completed per net (2 * agent + net): the epoch counter
+  uint32_t ep_pending;  // episodes finished in the running rollout (the last workgroup folds it in)
+  uint32_t pad1;
 };

@@ -23,7 +23,7 @@ class Engine:
     def __init__(self, obs_dims, local_q=None, *, num_units=64, batch_size=1024, max_episode_len=25,
                  capacity=int(1e6), num_envs=0, scenario="none", num_adversaries=0, lr=1e-2,
                  gamma=0.95, tau=1e-2, grad_clip=0.5, actor_reg=1e-3, adam_b1=0.9, adam_b2=0.999,
-                 adam_eps=1e-8, seed=0, world_size=1, rank=0, device=None):
+                 adam_eps=1e-8, seed=0, world_size=1, rank=0, device=None, episode_log_rows=0):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise RuntimeError("maddpg_amd runs on a ROCm GPU only (no CPU fallback)")
@@ -59,6 +59,7 @@ class Engine:
         cfg.adam_b1, cfg.adam_b2, cfg.adam_eps = adam_b1, adam_b2, adam_eps
         cfg.gamma = float(gamma)
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        cfg.episode_log_rows = int(episode_log_rows)
         self.cfg = cfg
         pt = ctypes.c_int64()
         nbytes = self.lib.mdp_arena_bytes(ctypes.byref(cfg), ctypes.byref(pt))
@@ -90,7 +91,7 @@ class Engine:
                 for t in range(6):
                     ti = MdpTensorInfo()
                     self._c("mdp_tensor", i, net, t, ctypes.byref(ti))
-                    infos.append((ti.offset, ti.rows, ti.cols))
+                    infos.append((ti.offset, ti.rows, ti.cols, ti.dev_rows, ti.dev_cols))
                 self._tensors[(i, net)] = infos
 
     # ------------------------------------------------------------ plumbing
@@ -137,13 +138,13 @@ class Engine:
         """float32 view of one net's gradient in the GRAD region (all-reduce target)."""
         infos = self._tensors[(agent, net)]
         start = infos[0][0]
-        end = infos[5][0] + ((infos[5][1] * infos[5][2] + 3) // 4) * 4
+        end = infos[5][0] + ((infos[5][3] * infos[5][4] + 3) // 4) * 4
         return self.region("grad")[start:end]
 
     # ---------------------------------------------------------- parameters
     def _flat_shapes(self, agent, which):
         net = 1 if "critic" in which else 0
-        return [(r, c) for (_o, r, c) in self._tensors[(agent, net)]]
+        return [(r, c) for (_o, r, c, _dr, _dc) in self._tensors[(agent, net)]]
 
     def set_params(self, agent, which, params):
         shapes = self._flat_shapes(agent, which)
@@ -430,6 +431,26 @@ class Engine:
             import sys
             print(f"[rank {rank}] xGMI exchange unavailable ({err}); using RCCL", file=sys.stderr)
         return ok
+
+    DP_KINDS = {0: None, 1: "rccl", 2: "xgmi"}
+
+    def dp_info(self):
+        """{kind, ranks, rank, peers}: the communicator this rank's gradient
+        exchange runs over (mdp_dp_info)."""
+        out = (ctypes.c_int32 * 4)()
+        self._c("mdp_dp_info", out)
+        return {"kind": self.DP_KINDS[out[0]], "ranks": out[1], "rank": out[2], "peers": out[3]}
+
+    def param_checksum(self):
+        """exact fingerprint of every replicated state region (weights, targets,
+        Adam moments, beta powers): int64 sums of the raw 32-bit words, plus a
+        position-weighted sum so permutations differ"""
+        out = []
+        for name in ("theta", "target", "adam_m", "adam_v", "beta"):
+            w = self.region(name, torch.int32).to(torch.int64)
+            pos = torch.arange(1, w.numel() + 1, device=w.device, dtype=torch.int64)
+            out += [int(w.sum().item()), int(((w & 0xFFFF) * pos).sum().item())]
+        return out
 
     def set_graphs(self, on=True):
         """hipGraph replay of update_round (default on; per-kernel profiling runs eager)."""

@@ -10,8 +10,13 @@ target actors + target critic + fp64 TD target (``:180-187``), critic step
 then critic (``:193-194``).  ``update`` returns the 6 stats of ``:196`` as a
 lazy sequence that synchronises only when read.
 
-``model`` is accepted for signature parity: the network is the reference's
-``mlp_model`` (2 hidden ReLU layers of ``args.num_units``, ``train.py:39-46``).
+``model`` must be the reference's ``mlp_model`` (``train.py:39-46``: two
+hidden ReLU layers of ``args.num_units`` and a linear output, TF
+``fully_connected`` with Xavier-uniform weights) -- the architecture the HIP
+kernels implement, for any ``--num-units`` up to 256.  It is recognised by name
+(the reference's own function, or :func:`mlp_model` below), ``None`` selects
+it; any other callable raises ``NotImplementedError`` rather than silently
+training a different network.
 """
 import numpy as np
 import torch
@@ -19,6 +24,25 @@ import torch
 from .. import AgentTrainer
 from ..common import tf_util as U
 from .replay_buffer import ReplayBuffer
+
+
+MAX_UNITS = 256
+
+
+def mlp_model(input, num_outputs, scope, reuse=False, num_units=64, rnn_cell=None):
+    """The reference's model function (``experiments/train.py:39-46``), kept as
+    the architecture marker: the network itself is built by the device engine."""
+    raise NotImplementedError("mlp_model is realised by the MI355X kernels; pass it to MADDPGAgentTrainer")
+
+
+def check_model(model, num_units):
+    """``model`` must describe the reference's mlp_model (see module doc)."""
+    if model is not None and getattr(model, "__name__", None) != "mlp_model":
+        raise NotImplementedError(
+            f"model {model!r} is not mlp_model: the MI355X kernels implement the reference's 2-hidden-layer "
+            "ReLU MLP (experiments/train.py:39-46) only")
+    if not 1 <= int(num_units) <= MAX_UNITS:
+        raise ValueError(f"--num-units {num_units}: the kernels take 1..{MAX_UNITS} hidden units")
 
 
 class UpdateStats(object):
@@ -62,6 +86,7 @@ class MADDPGAgentTrainer(AgentTrainer):
         self.obs_shape_n = [tuple(s) for s in obs_shape_n]
         self.act_space_n = act_space_n
         self.local_q_func = local_q_func
+        check_model(model, args.num_units)
         for sp in act_space_n:
             if getattr(sp, "n", 5) != 5:
                 raise NotImplementedError("only Discrete(5) MPE action spaces are supported")

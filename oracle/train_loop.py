@@ -100,7 +100,7 @@ def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, m
     el = time.perf_counter() - t0
     return {"env_steps_per_sec": env_steps / el, "trainer_updates_per_sec": updates / el,
             "env_steps": env_steps, "updates": updates, "seconds": el, "scenario": scenario,
-            "batch_size": batch_size, "num_units": num_units, "prefill": prefill}
+            "batch_size": batch_size, "num_units": num_units, "prefill": prefill, "n_agents": n}
 
 
 def main():

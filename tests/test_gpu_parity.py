@@ -539,7 +539,8 @@ def test_env_episode_reset_and_log():
     rows = eng.replay_rows(0, 3 * E).cpu().numpy()
     lay, _ = row_layout(sp.obs_dims)
     per_env = sum(rows[k * E:(k + 1) * E, lay[j]["rew"]] for k in range(3) for j in range(3))
-    np.testing.assert_allclose(np.sort(log[:, 0]), np.sort(per_env), rtol=1e-5, atol=1e-4)
+    # lockstep envs log in env order (slot = episodes + env index)
+    np.testing.assert_allclose(log[:, 0], per_env, rtol=1e-5, atol=1e-4)
     np.testing.assert_allclose(log[:, 0], log[:, 1:].sum(1), rtol=1e-5, atol=1e-4)
 
 

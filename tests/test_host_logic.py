@@ -15,7 +15,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     assert set(_lib.SIGNATURES) <= set(syms)
-    assert lib.mdp_abi_version() == 1
+    assert lib.mdp_abi_version() == _lib.ABI_VERSION == 2
 
 
 def _cfg(**kw):
@@ -40,7 +40,15 @@ def test_arena_size_and_config_validation():
     assert pt.value >= 3 * (5701 + 8705) and pt.value < 3 * (5701 + 8705) + 3 * 12 * 4
     # replay 1e6 rows x 132 floats dominates
     assert nb > 4 * 1_000_000 * 132
-    assert lib.mdp_arena_bytes(ctypes.byref(_cfg(num_units=96)), None) < 0      # H must be 64/128
+    # any --num-units the reference takes (train.py:24) up to 256: the device
+    # nets are padded to the kernel width 64 / 128 / 256
+    for u, dev in [(1, 64), (32, 64), (64, 64), (96, 128), (128, 128), (200, 256), (256, 256)]:
+        pu = ctypes.c_int64()
+        assert lib.mdp_arena_bytes(ctypes.byref(_cfg(num_units=u)), ctypes.byref(pu)) > 0
+        per_agent = (18 * dev + dev + dev * dev + dev + dev * 5 + 8) + (69 * dev + dev + dev * dev + dev + dev + 4)
+        assert pu.value == 3 * per_agent, (u, pu.value)
+    assert lib.mdp_arena_bytes(ctypes.byref(_cfg(num_units=0)), None) < 0
+    assert lib.mdp_arena_bytes(ctypes.byref(_cfg(num_units=257)), None) < 0
     assert lib.mdp_arena_bytes(ctypes.byref(_cfg(act_dim=4)), None) < 0
     bad = _cfg()
     bad.obs_dim[1] = 17                                                          # not simple_spread
@@ -157,3 +165,88 @@ def test_oracle_benchmark_records():
         raise AssertionError("simple has no benchmark_data")
     except AttributeError:
         pass
+
+
+def _reference_curve(rewards, save_rate, num_episodes):
+    """experiments/train.py:123-189 with episodes ending one at a time: the
+    episode_rewards list, the save_rate check after each reset, the stop."""
+    import numpy as np
+    ep = [0.0]
+    curve = []
+    for r in rewards:
+        ep[-1] += r
+        ep.append(0.0)                                   # reset (:127-133)
+        if len(ep) % save_rate == 0:                     # :164
+            curve.append(float(np.mean(ep[-save_rate:])))
+        if len(ep) > num_episodes:                       # :181
+            break
+    return curve, len(ep)
+
+
+@pytest.mark.parametrize("E,save_rate,num_episodes", [(1, 1000, 5000), (64, 100, 300), (4096, 1000, 20000),
+                                                      (5, 3, 40), (7, 1, 20), (1024, 1000, 3000)])
+def test_learning_curve_cadence_matches_reference(E, save_rate, num_episodes):
+    """E env copies terminating together give the reference's curve: one point
+    per save_rate multiple crossed (several per step when E > save_rate), each
+    the mean over the last save_rate entries incl. the fresh 0, up to the
+    length the reference stops at."""
+    import numpy as np
+    from experiments.train import LearningCurve
+    rng = np.random.default_rng(E + save_rate)
+    total = num_episodes + 2 * E
+    rewards = rng.normal(-30, 5, size=total).astype(np.float32)
+    want, final_len = _reference_curve(rewards.astype(np.float64), save_rate, num_episodes)
+    lc = LearningCurve(save_rate, num_episodes, 1)
+    log = np.stack([rewards, rewards], 1)
+    got = []
+    while not lc.done:
+        pts = lc.finish(E, lambda first, count: log[first:first + count])
+        got += [p[1] for p in pts]
+    assert len(got) == len(want) == final_len // save_rate - 1 // save_rate
+    np.testing.assert_allclose(got, want, rtol=1e-6)
+    assert lc.final_ep_rewards == got and len(lc.final_ep_ag_rewards) == len(got)
+
+
+def test_model_must_be_mlp_model():
+    import types
+    from maddpg_amd.trainer.maddpg import check_model, mlp_model
+
+    def mlp_model_ref(input, num_outputs, scope, reuse=False, num_units=64, rnn_cell=None):
+        pass
+    mlp_model_ref.__name__ = "mlp_model"          # the reference's own function (train.py:39)
+    for m in (None, mlp_model, mlp_model_ref):
+        check_model(m, 64)
+    with pytest.raises(NotImplementedError, match="mlp_model"):
+        check_model(lambda x, n, s: x, 64)
+    with pytest.raises(NotImplementedError):
+        check_model(types.SimpleNamespace(), 64)
+    with pytest.raises(ValueError):
+        check_model(mlp_model, 300)
+
+
+def test_optimizer_coresidency_plan():
+    """mdp_ra_plan: the fused optimizer launch (chunk workgroups spin on each
+    other's norm partials / the xGMI peers) is used only when its whole grid is
+    co-resident; otherwise that net falls back to k_reduce + k_apply.  MI355X:
+    256 CUs x 1 workgroup of 1024 threads (k_reduce_apply's occupancy)."""
+    lib = _lib.load()
+    out = (ctypes.c_int32 * 16)()
+    # S2 at H=64, chunks of 256 per tensor: critic W1 18 + b1 1 + W2 16 + b2 1 +
+    # W3 1 + b3 1 + stats 1 = 39; actor 5 + 1 + 16 + 1 + 2 + 1 = 26, + 13 Polyak
+    # workgroups of the critic (1,024-parameter chunks) + stats = 40 (3 agents)
+    assert lib.mdp_ra_plan(ctypes.byref(_cfg()), 256, 1, out) == 0
+    assert list(out[:6]) == [40, 39] * 3
+    # the same launch on a device holding 39 workgroups: the actor steps fall back
+    assert lib.mdp_ra_plan(ctypes.byref(_cfg()), 39, 1, out) == 3
+    assert list(out[:6]) == [-40, 39] * 3
+    # H=256: the 256x256 W2 alone is 256 chunks -> every critic step (330
+    # workgroups) and actor step exceed 256 slots
+    n = lib.mdp_ra_plan(ctypes.byref(_cfg(num_units=256)), 256, 1, out)
+    assert n == 6 and all(v < 0 for v in out[:6]) and -out[1] > 256
+    # configs[4] topology (tag N=6, H=128): every net fits on one MI355X
+    tag = _cfg(n_agents=6, num_units=128, scenario=4, num_adversaries=4)
+    for i, d in enumerate([22, 22, 22, 22, 20, 20]):
+        tag.obs_dim[i] = d
+    assert lib.mdp_ra_plan(ctypes.byref(tag), 256, 1, out) == 0
+    assert max(out[:12]) <= 256
+    assert lib.mdp_ra_plan(ctypes.byref(_cfg(num_units=0)), 256, 1, out) < 0

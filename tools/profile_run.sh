@@ -9,12 +9,12 @@ export TMPDIR=/tmp
 O=gpurun_out/$TAG
 rm -rf $O; mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
-    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-throughput-figure --no-gather-stage > $O/prof_bench.json 2> $O/prof_bench.err
+    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-throughput-figure --no-gather-stage --no-configs2 > $O/prof_bench.json 2> $O/prof_bench.err
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage > $O/fetch.json 2> $O/fetch.err
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage --no-configs2 > $O/fetch.json 2> $O/fetch.err
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage > $O/write.json 2> $O/write.err
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage --no-configs2 > $O/write.json 2> $O/write.err
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/mfma -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage > $O/mfma.json 2> $O/mfma.err
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage --no-configs2 > $O/mfma.json 2> $O/mfma.err
 echo "profile $TAG done"
