@@ -63,6 +63,8 @@ def parse_args(argv=None):
     parser.add_argument("--num-agents", type=int, default=None, help="scenario agent count override")
     parser.add_argument("--scenario-adversaries", type=int, default=None, help="adversaries in the scenario world")
     parser.add_argument("--train-every", type=int, default=100, help="transitions per update round (maddpg.py:164)")
+    parser.add_argument("--display-frames", type=int, default=100,
+                        help="--display: steps rendered to PNG frames (no window on a GPU box)")
     parser.add_argument("--update-mode", choices=["strict", "throughput"], default="strict",
                         help="strict: the reference's update order; throughput: every agent's gradients from "
                              "the round-start parameters, then every optimizer step (SURVEY 8e, single GPU)")
@@ -163,14 +165,30 @@ def benchmark(arglist, runner, exp_name, rank):
     return runner
 
 
+def display(arglist, runner, exp_name, rank):
+    """--display (train.py:150-154): the loaded policies act, nothing trains,
+    every step is rendered.  Headless: env copy 0 is rasterised to
+    <plots-dir><exp-name>_display/frame_NNNNN.png (+ positions.npz) for
+    --display-frames steps (the reference loops until interrupted)."""
+    from maddpg_amd.render import FrameWriter
+    out = FrameWriter(os.path.join(arglist.plots_dir, exp_name + "_display"), runner.spec)
+    for _ in range(arglist.display_frames):
+        runner.rollout()                                   # action_n, env.step, reset at terminal
+        if rank == 0:
+            st = runner.eng.env_state()
+            out.add(st["pos"][0], st["goal"][0])
+    if rank == 0:
+        print(f"Rendered {out.close()} frames to {out.dir}", flush=True)
+    runner.synchronize()
+    return runner
+
+
 def train(arglist):
     import torch
 
     from maddpg_amd.parallel import init_process_group_from_env
     from maddpg_amd.runner import VecRunner
 
-    if arglist.display:
-        raise SystemExit("--display needs MPE's pyglet viewer, which this build does not ship")
     exp_name = arglist.exp_name if arglist.exp_name is not None else arglist.scenario
     world, rank, local = init_process_group_from_env()
     if torch.cuda.is_available():
@@ -193,11 +211,13 @@ def train(arglist):
 
     if arglist.load_dir == "":
         arglist.load_dir = arglist.save_dir
-    if arglist.restore or arglist.benchmark:                  # train.py:92-96
+    if arglist.restore or arglist.benchmark or arglist.display:   # train.py:92-96
         say('Loading previous state...')
         runner.eng.load_state(arglist.load_dir)
     if arglist.benchmark:
         return benchmark(arglist, runner, exp_name, rank)
+    if arglist.display:
+        return display(arglist, runner, exp_name, rank)
 
     E, L = arglist.num_envs, arglist.max_episode_len
     curve = LearningCurve(arglist.save_rate, arglist.num_episodes, n)

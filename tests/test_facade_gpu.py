@@ -171,3 +171,41 @@ def test_train_cli_benchmark_mode(tmp_path, capsys, scenario, extra):
     assert [len(ep[0]) for ep in info] == [4, 5, 5]
     assert all(len(ep) == 1 for ep in info)
     assert all(len(step) == r.n for ep in info for step in ep[0])
+
+
+def test_train_cli_curve_cadence_many_envs(tmp_path, capsys):
+    """--num-envs > --save-rate: every save_rate multiple crossed by one vector
+    step is one print and one curve point (train.py:164-178), up to the length
+    the reference stops at; the curve equals LearningCurve over the episode log."""
+    import pickle
+    from experiments.train import parse_args, train
+    a = parse_args(["--scenario", "simple_spread", "--num-envs", "256", "--num-episodes", "1000",
+                    "--save-rate", "100", "--batch-size", "64", "--max-episode-len", "5",
+                    "--save-dir", str(tmp_path) + "/", "--plots-dir", str(tmp_path) + "/", "--exp-name", "c"])
+    runner = train(a)
+    out = capsys.readouterr().out
+    curve = pickle.load(open(str(tmp_path) + "/c_rewards.pkl", "rb"))
+    # the reference stops at len(episode_rewards) = 1001: points at 100, 200, ..., 1000
+    assert len(curve) == 10 and out.count("mean episode reward") == 10
+    assert len(pickle.load(open(str(tmp_path) + "/c_agrewards.pkl", "rb"))) == 10 * 3
+    log = runner.episode_rewards(0, 999)
+    want = [float(np.sum(log[m - 100:m - 1, 0], dtype=np.float64) / 100) for m in range(100, 1001, 100)]
+    np.testing.assert_allclose(curve, want, rtol=1e-6)
+
+
+def test_train_cli_display_headless(tmp_path, capsys):
+    """--display (train.py:150-154): loads the saved policies, steps without
+    training, renders env copy 0 to PNG frames."""
+    from experiments.train import parse_args, train
+    common = ["--scenario", "simple_adversary", "--num-adversaries", "1", "--batch-size", "64",
+              "--max-episode-len", "5", "--save-dir", str(tmp_path) + "/", "--plots-dir", str(tmp_path) + "/"]
+    train(parse_args(common + ["--num-envs", "64", "--num-episodes", "100", "--save-rate", "50", "--exp-name", "t"]))
+    capsys.readouterr()
+    r = train(parse_args(common + ["--display", "--display-frames", "7", "--exp-name", "v"]))
+    out = capsys.readouterr().out
+    assert "Loading previous state..." in out and "Rendered 7 frames" in out
+    assert r.rounds == 0
+    d = os.path.join(str(tmp_path), "v_display")
+    assert sorted(os.listdir(d))[:2] == ["frame_00000.png", "frame_00001.png"]
+    pos = np.load(os.path.join(d, "positions.npz"))["pos"]
+    assert pos.shape == (7, 5, 2) and np.all(np.isfinite(pos))

@@ -250,3 +250,36 @@ def test_optimizer_coresidency_plan():
     assert lib.mdp_ra_plan(ctypes.byref(tag), 256, 1, out) == 0
     assert max(out[:12]) <= 256
     assert lib.mdp_ra_plan(ctypes.byref(_cfg(num_units=0)), 256, 1, out) < 0
+
+
+def test_headless_display_frames(tmp_path):
+    """--display's renderer (train.py:150-154, MPE env.render without a window):
+    PNG frames that decode to the right size with the entities drawn."""
+    import struct
+    import zlib
+
+    import numpy as np
+    from maddpg_amd.render import FrameWriter, entity_table, rasterize
+    for name, n, na in [("simple", None, None), ("simple_spread", None, None), ("simple_adversary", None, None),
+                        ("simple_tag", 6, 4)]:
+        sp = spec(name, n, na)
+        tab = entity_table(sp)
+        assert len(tab) == sp.n_agents + {"simple": 1, "simple_spread": sp.n_agents,
+                                          "simple_adversary": sp.n_agents - 1, "simple_tag": 2}[name]
+    sp = spec("simple_spread")
+    pos = np.array([[0.0, 0.0], [0.5, 0.5], [-0.5, -0.5], [0.9, -0.9], [-0.9, 0.9], [0.0, 0.6]], np.float32)
+    img = rasterize(pos, entity_table(sp), px=200)
+    assert img.shape == (200, 200, 3)
+    assert tuple(img[100, 100]) == (89, 89, 217)          # agent 0 at the centre, MPE agent colour
+    assert tuple(img[0, 0]) == (255, 255, 255)
+    w = FrameWriter(str(tmp_path / "d"), sp)
+    for k in range(3):
+        w.add(pos + 0.01 * k)
+    assert w.close() == 3
+    raw = open(tmp_path / "d" / "frame_00002.png", "rb").read()
+    assert raw[:8] == b"\x89PNG\r\n\x1a\n"
+    wdt, hgt = struct.unpack(">II", raw[16:24])
+    assert (wdt, hgt) == (256, 256)
+    idat = raw[raw.index(b"IDAT") + 4: raw.index(b"IEND") - 8]
+    assert len(zlib.decompress(idat)) == hgt * (1 + 3 * wdt)
+    assert np.load(tmp_path / "d" / "positions.npz")["pos"].shape == (3, 6, 2)
