@@ -205,7 +205,8 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   // per-agent blocks of partial gradients / stats / TD targets (throughput mode
   // computes every agent's gradients in one launch; strict mode uses block 0)
   sz[MDP_R_SLAB] = (int64_t)n * (4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg +
-                                  8 * (int64_t)c->batch_size) + 256 + 256 + mdp_ra_sync_bytes();
+                                  8 * (int64_t)c->batch_size) + 256 + 256 + mdp_ra_sync_bytes() +
+                   4 * (int64_t)L.nwg * 16 * MDP_APRE_W;  // the precomputed actor forward (16 rows per tile)
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
   for (int r = 0; r < MDP_R_COUNT; ++r) {
@@ -286,6 +287,10 @@ struct mdp_handle {
   bool fused_apply = true;
   uint32_t* ra_ctr = nullptr;
   uint64_t* ra_part = nullptr;
+  // the actor forward + sample of agent i computed by extra workgroups of its
+  // critic-step launch (fast kernels, strict order; MDP_ACTOR_PRE=0: off)
+  float* apre = nullptr;
+  bool actor_pre = true;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
   // mdp_train_step graphs (rollout + k rounds), one per k
@@ -437,8 +442,10 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
 // partials / stats / TD targets and noise counter upd_ctr + agent (multi = 2
 // marks it; the general kernels take the agent from a.agent, not the grid)
 int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr,
-                   bool tp = false) {
+                   bool tp = false, bool apre = false, const float* u_act = nullptr) {
   CriticArgs a;
+  a.apre = nullptr;
+  a.u_act = u_act;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.pf_ctl = h->ctl;
@@ -471,6 +478,7 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
       a.pf_out = pf_out;
       a.pf_count = h->cfg.n_agents * h->cfg.batch_size;
     }
+    if (apre) a.apre = h->apre;
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
     return 0;
   }
@@ -484,8 +492,10 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   return 0;
 }
 
-int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, bool tp = false) {
+int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, bool tp = false,
+                  bool apre = false) {
   ActorArgs a;
+  a.apre = apre ? h->apre : nullptr;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.topo = h->L.topo;
@@ -697,22 +707,30 @@ int dp_allreduce_all(mdp_handle* h) {
   return 0;
 }
 
+// the critic step's launch also computes the actor step's forward + sample
+// (extra workgroups on the otherwise idle CUs; the actor weights are not
+// touched by the critic step, the indices and noise are the actor step's own)
+bool actor_pre_ok(const mdp_handle* h, int agent) {
+  return h->actor_pre && !h->general_grads && grads_r_ok(h->L.topo, agent);
+}
+
 // strict data-parallel update of one agent (maddpg.py:188-194 order):
 // critic grads -> reduce -> all-reduce -> clip + Adam (x 1/G); then the actor
 int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out) {
   const float scale = 1.0f / (float)h->dp_world;
+  const bool pre = actor_pre_ok(h, agent);
   int rc;
   if (h->p2p) {  // the exchange lives inside the optimizer launch: same 4 launches as one GPU
-    if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out))) return rc;
+    if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre))) return rc;
     if ((rc = do_reduce_apply(h, agent, 1))) return rc;
-    if ((rc = do_actor_grad(h, agent, idx, nullptr))) return rc;
+    if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre))) return rc;
     return do_reduce_apply(h, agent, 0);
   }
-  if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre))) return rc;
   if ((rc = do_reduce(h, agent, 1))) return rc;
   if ((rc = dp_allreduce(h, agent, 1))) return rc;
   if ((rc = do_apply(h, agent, 1, false, scale))) return rc;
-  if ((rc = do_actor_grad(h, agent, idx, nullptr))) return rc;
+  if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre))) return rc;
   if ((rc = do_reduce(h, agent, 0))) return rc;
   if ((rc = dp_allreduce(h, agent, 0))) return rc;
   return do_apply(h, agent, 0, false, scale);
@@ -724,14 +742,15 @@ int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, 
   if ((h->comm || h->p2p) && !u_tgt && !u_act) return do_update_dp(h, agent, idx, pf_out);
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
-  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out))) return rc;
+  const bool pre = actor_pre_ok(h, agent);
+  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act))) return rc;
   if (fused) {
     if ((rc = do_reduce_apply(h, agent, 1))) return rc;
   } else {
     if ((rc = do_reduce(h, agent, 1))) return rc;
     if ((rc = do_apply(h, agent, 1, false, 1.0f))) return rc;
   }
-  if ((rc = do_actor_grad(h, agent, idx, u_act))) return rc;
+  if ((rc = do_actor_grad(h, agent, idx, u_act, false, pre))) return rc;
   if (fused) {
     if ((rc = do_reduce_apply(h, agent, 0))) return rc;
   } else {
@@ -830,6 +849,8 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
   for (int i = 0; i < n; ++i) lds_c = std::max(lds_c, lds_critic_r_bytes(h->L.topo, i));
   {
     CriticArgs a;
+    a.apre = nullptr;
+    a.u_act = nullptr;
     a.pf_ctl = h->ctl;
     a.pf_out = pf_out;
     a.pf_count = pf_out ? n * h->cfg.batch_size : 0;
@@ -857,6 +878,7 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
   }
   {
     ActorArgs a;
+    a.apre = nullptr;
     a.topo = h->L.topo;
     a.agent = 0;
     a.B = h->cfg.batch_size;
@@ -985,6 +1007,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->fused_apply = !(u && u[0] == '1');
     const char* rd = getenv("MDP_ROLLOUT_DRAW");
     h->rollout_draw = !(rd && rd[0] == '0');
+    const char* ap = getenv("MDP_ACTOR_PRE");
+    h->actor_pre = !(ap && ap[0] == '0');
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
@@ -1051,6 +1075,7 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     p = (char*)(((uintptr_t)p + 255) & ~uintptr_t(255));
     h->ra_ctr = (uint32_t*)p;
     h->ra_part = (uint64_t*)(p + (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128);
+    h->apre = (float*)(p + mdp_ra_sync_bytes());
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
   std::vector<float> beta(8 * cfg->n_agents);

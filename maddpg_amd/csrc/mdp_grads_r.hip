@@ -119,6 +119,94 @@ __device__ __forceinline__ void dw3a_store(const float* gwpart, const float* dl,
     slab_st(db3 + lane, s);
   }
 }
+// actor forward of 16 rows on ONE wave (maddpg.py:39) and the fresh policy
+// sample a_i (:49): h1a, h2a (LDS, stride LH), logits lg and sample av (stride
+// 8).  Weights and the Gumbel noise are requested before waiting for the
+// replay rows (nsig gather waves signal rows_ready).
+__device__ __forceinline__ void actor_fwd_wave(const float* __restrict__ P, const NDesc& na, const ADesc& ag,
+                                               const float* rowbuf, int ldr, const float* u_act, int nvalid, int r0,
+                                               uint64_t seed, int agent, uint32_t ctr, int* rows_ready, int nsig,
+                                               float* h1a, float* h2a, float* lg, float* av) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  f32x4 w1[16], w2[16];
+  float w3[16];
+  rf_load<16>(w1, P + na.t[0].off, ag.obs_dim, 0, 0);
+  rf_load<16>(w2, P + na.t[2].off, RH, 0, 0);
+  rh_load(w3, P + na.t[4].off, MDP_ACT_DIM);
+  const f32x4 b1 = ld4(P + na.t[1].off + 4 * r), b2 = ld4(P + na.t[3].off + 4 * r);
+  const float b3 = P[na.t[5].off + min(r, MDP_ACT_DIM - 1)];
+  float gn[MDP_ACT_DIM];  // Gumbel noise of the policy sample, while the weights are in flight
+  {
+    float u[MDP_ACT_DIM];
+    if (u_act) {
+      for (int k = 0; k < MDP_ACT_DIM; ++k) u[k] = lane < nvalid ? u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
+    } else {
+      uniforms5(seed, (uint32_t)((agent << 8) | 0x80), ctr, (uint32_t)(r0 + (lane & 15)), u);
+    }
+    gumbel_noise5(u, gn);
+  }
+  lds_wait(rows_ready, nsig);
+  MDP_STAMP(17);
+  {
+    f32x4 acc[4];
+    rf_zero(acc);
+    rf_acc<16>(acc, rowbuf + ag.obs_off, ldr, ag.obs_dim, w1);
+    rf_store<true>(acc, b1, h1a, LH);
+  }
+  wave_sync();
+  {
+    f32x4 acc[4];
+    rf_zero(acc);
+    rf_acc<16>(acc, h1a, LH, RH, w2);
+    rf_store<true>(acc, b2, h2a, LH);
+  }
+  wave_sync();
+  {
+    const f32x4 acc = rh_acc(h2a, LH, w3);
+    if (r < MDP_ACT_DIM) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lg[(kq * 4 + i) * 8 + r] = acc[i] + b3;
+    }
+  }
+  wave_sync();
+  if (lane < MDP_R) gumbel_softmax5_pre(lg + lane * 8, gn, av + lane * 8);
+}
+
+// float4 q of a row block [16][MDP_APRE_W] <-> its LDS home (h1a | h2a | lg | av)
+__device__ __forceinline__ float* apre_lds(int q, float* h1a, float* h2a, float* lg, float* av) {
+  const int row = q / (MDP_APRE_W / 4), c = 4 * (q - row * (MDP_APRE_W / 4));
+  return c < 64 ? h1a + row * LH + c : c < 128 ? h2a + row * LH + c - 64 : c < 136 ? lg + row * 8 + c - 128
+                                                                                  : av + row * 8 + c - 136;
+}
+
+// extra workgroup of k_critic_grad_r: the actor forward + sample of row tile bx
+// for the actor step that follows (same agent, same indices, same noise)
+__device__ __forceinline__ void actor_pre_tile(const CriticArgs& a, float* lds, int* rows_ready, int bx) {
+  const Topo& T = a.topo;
+  const ADesc& ag = T.ag[a.agent];
+  const int ldr = lds_ld(T.row_stride);
+  LdsCarve cv(lds);
+  float* rowbuf = cv.take(MDP_R * ldr);
+  float* h1a = cv.take(MDP_R * LH);
+  float* h2a = cv.take(MDP_R * LH);
+  float* lg = cv.take(MDP_R * 8);
+  float* av = cv.take(MDP_R * 8);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r0 = bx * MDP_R, nvalid = min(MDP_R, a.B - r0);
+  if (threadIdx.x == 0) *rows_ready = 0;
+  __syncthreads();
+  if (wave == 0) {
+    actor_fwd_wave(a.theta, ag.actor, ag, rowbuf, ldr, a.u_act, nvalid, r0, a.seed, a.agent, a.ctl->upd_ctr,
+                   rows_ready, 7, h1a, h2a, lg, av);
+  } else {
+    gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 64, 448);
+    lds_signal(rows_ready);
+  }
+  __syncthreads();
+  float* dst = a.apre + (int64_t)r0 * MDP_APRE_W;
+  for (int q = threadIdx.x; q < MDP_R * MDP_APRE_W / 4; q += blockDim.x)
+    *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(apre_lds(q, h1a, h2a, lg, av));
+}
 }  // namespace
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
@@ -131,6 +219,13 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;  // gather waves done (LDS hand-off, replaces a barrier)
   int agent = a.agent, bx = blockIdx.x;
+  if (a.apre) {  // workgroups [B/16, 2 B/16): the actor step's forward (strict mode only)
+    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    if (bx >= nwg) {
+      actor_pre_tile(a, lds, &rows_ready, bx - nwg);
+      return;
+    }
+  }
   if (a.multi > 1) {  // throughput mode: every agent's critic step in this launch
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
     agent = bx / nwg;
@@ -462,49 +557,21 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   if (wave < 4) {
     if (wave == 0) {
       // ---------------- actor forward on obs_i -> logits p (maddpg.py:39), sample a_i (:49)
-      f32x4 w1[16], w2[16], wda[4];
-      float w3[16], w3a[MDP_ACT_DIM];
-      rf_load<16>(w1, P + na.t[0].off, ag.obs_dim, 0, 0);
-      rf_load<16>(w2, P + na.t[2].off, RH, 0, 0);
-      rh_load(w3, P + na.t[4].off, MDP_ACT_DIM);
-      const f32x4 b1 = ld4(P + na.t[1].off + 4 * r), b2 = ld4(P + na.t[3].off + 4 * r);
-      const float b3 = P[na.t[5].off + min(r, MDP_ACT_DIM - 1)];
-      float gn[MDP_ACT_DIM];  // Gumbel noise of the policy sample, while the weights are in flight
-      {
-        float u[MDP_ACT_DIM];
-        if (u_act) {
-          for (int k = 0; k < MDP_ACT_DIM; ++k)
-            u[k] = lane < nvalid ? u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
-        } else {
-          uniforms5(a.seed, (uint32_t)((agent << 8) | 0x80), ctr, (uint32_t)(r0 + (lane & 15)), u);
-        }
-        gumbel_noise5(u, gn);
-      }
-      lds_wait(&rows_ready, 6);
-      MDP_STAMP(17);
-      {
-        f32x4 acc[4];
-        rf_zero(acc);
-        rf_acc<16>(acc, rowbuf + ag.obs_off, ldr, ag.obs_dim, w1);
-        rf_store<true>(acc, b1, h1a, LH);
-      }
-      wave_sync();
-      {
-        f32x4 acc[4];
-        rf_zero(acc);
-        rf_acc<16>(acc, h1a, LH, RH, w2);
-        rf_store<true>(acc, b2, h2a, LH);
-      }
-      wave_sync();
-      {
-        const f32x4 acc = rh_acc(h2a, LH, w3);
-        if (r < MDP_ACT_DIM) {
+      f32x4 wda[4];
+      float w3a[MDP_ACT_DIM];
+      if (a.apre) {  // computed by the critic launch's extra workgroups: load the block
+        const float* src = a.apre + (int64_t)r0 * MDP_APRE_W;
+        f32x4 v[MDP_APRE_W / 16];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) lg[(kq * 4 + i) * 8 + r] = acc[i] + b3;
-        }
+        for (int k = 0; k < MDP_APRE_W / 16; ++k) v[k] = ld4(src + 4 * (lane + 64 * k));
+#pragma unroll
+        for (int k = 0; k < MDP_APRE_W / 16; ++k)
+          *reinterpret_cast<f32x4*>(apre_lds(lane + 64 * k, h1a, h2a, lg, av)) = v[k];
+        wave_sync();
+      } else {
+        actor_fwd_wave(P, na, ag, rowbuf, ldr, u_act, nvalid, r0, a.seed, agent, ctr, &rows_ready, 6, h1a, h2a, lg,
+                       av);
       }
-      wave_sync();
-      if (lane < MDP_R) gumbel_softmax5_pre(lg + lane * 8, gn, av + lane * 8);
       // backward-phase weights: W1c rows of the a_i input (for da) and W3 of the actor (for d2a)
       rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
 #pragma unroll
@@ -657,7 +724,9 @@ hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr, int 
 
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s) {
   static bool attr = false;
-  return launch_r(k_critic_grad_r, a, lds_bytes, s, attr, a.pf_count > 0 ? 1 : 0);
+  const int per = (a.B + MDP_R - 1) / MDP_R;
+  // grid: critic row tiles | actor-forward row tiles (a.apre) | the index draw (pf_count; last)
+  return launch_r(k_critic_grad_r, a, lds_bytes, s, attr, (a.apre ? per : 0) + (a.pf_count > 0 ? 1 : 0));
 }
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s) {
   static bool attr = false;

@@ -32,7 +32,17 @@ struct CriticArgs {
   // per-agent strides and the noise counter is upd_ctr + agent
   int multi;
   int64_t slab_agent_stride;
+  // k_critic_grad_r only: B/16 extra workgroups run the SAME agent's actor
+  // forward + policy sample of the coming actor step (it needs only the actor
+  // weights, which the critic step does not touch) into apre [B][MDP_APRE_W];
+  // u_act: injected uniforms of that sample or null (0: no extra workgroups)
+  float* apre;
+  const float* u_act;
 };
+
+// precomputed actor forward of one batch row (k_critic_grad_r's extra
+// workgroups -> k_actor_grad_r): h1 [64] | h2 [64] | logits [8] | sample [8]
+#define MDP_APRE_W 144
 
 struct ActorArgs {
   Topo topo;
@@ -50,6 +60,7 @@ struct ActorArgs {
   double* slab_stat;
   int multi;                  // throughput mode, as CriticArgs
   int64_t slab_agent_stride;
+  const float* apre;          // k_actor_grad_r: the forward precomputed by the critic launch, or null
 };
 
 struct ReduceArgs {
