@@ -206,7 +206,7 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   // computes every agent's gradients in one launch; strict mode uses block 0)
   sz[MDP_R_SLAB] = (int64_t)n * (4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg +
                                   8 * (int64_t)c->batch_size) + 256 + 256 + mdp_ra_sync_bytes() +
-                   4 * (int64_t)L.nwg * 16 * MDP_APRE_W;  // the precomputed actor forward (16 rows per tile)
+                   4 * (int64_t)L.nwg * 16 * (MDP_APRE_W + MDP_CPRE_W);  // precomputed actor / critic work
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
   for (int r = 0; r < MDP_R_COUNT; ++r) {
@@ -291,6 +291,11 @@ struct mdp_handle {
   // critic-step launch (fast kernels, strict order; MDP_ACTOR_PRE=0: off)
   float* apre = nullptr;
   bool actor_pre = true;
+  // the next agent's critic-step work independent of this agent's update,
+  // computed by extra workgroups of this agent's actor-step launch (critic_pre
+  // -> critic_post; fast kernels, strict order; MDP_CRITIC_PRE=0: off)
+  float* cpre = nullptr;
+  bool critic_pre = true;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
   // mdp_train_step graphs (rollout + k rounds), one per k
@@ -442,10 +447,12 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
 // partials / stats / TD targets and noise counter upd_ctr + agent (multi = 2
 // marks it; the general kernels take the agent from a.agent, not the grid)
 int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr,
-                   bool tp = false, bool apre = false, const float* u_act = nullptr) {
+                   bool tp = false, bool apre = false, const float* u_act = nullptr, int post_prev = -1) {
   CriticArgs a;
   a.apre = nullptr;
   a.u_act = u_act;
+  a.cpre = nullptr;
+  a.cpre_prev = post_prev;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.pf_ctl = h->ctl;
@@ -479,6 +486,7 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
       a.pf_count = h->cfg.n_agents * h->cfg.batch_size;
     }
     if (apre) a.apre = h->apre;
+    if (post_prev >= 0) a.cpre = h->cpre;
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
     return 0;
   }
@@ -493,9 +501,13 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
 }
 
 int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, bool tp = false,
-                  bool apre = false) {
+                  bool apre = false, int pre_next = -1, const int32_t* pre_idx = nullptr) {
   ActorArgs a;
   a.apre = apre ? h->apre : nullptr;
+  a.cpre = nullptr;
+  a.cpre_agent = pre_next;
+  a.cpre_idx = pre_idx;
+  a.target = h->target;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.topo = h->L.topo;
@@ -518,7 +530,12 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
   }
   ProfScope p(h, MDP_K_ACTOR_GRAD);
   if (!tp && !h->general_grads && grads_r_ok(h->L.topo, agent)) {
-    HIPCHK(h, mdp_launch_actor_grad_r(a, lds_actor_r_bytes(h->L.topo), h->stream));
+    int lds = lds_actor_r_bytes(h->L.topo);
+    if (pre_next >= 0) {
+      a.cpre = h->cpre;
+      lds = std::max(lds, lds_critic_pre_bytes(h->L.topo));
+    }
+    HIPCHK(h, mdp_launch_actor_grad_r(a, lds, h->stream));
     return 0;
   }
   HIPCHK(h, mdp_launch_actor_grad(a, h->L.topo.H, lds_actor_bytes(h->L.topo), h->stream));
@@ -714,43 +731,56 @@ bool actor_pre_ok(const mdp_handle* h, int agent) {
   return h->actor_pre && !h->general_grads && grads_r_ok(h->L.topo, agent);
 }
 
+// agent k's critic step split around agent p's update (critic_pre in p's actor
+// launch, critic_post for k): fast kernels for both, k's critic MADDPG-style
+// (a DDPG critic needs no target actor but its own)
+bool critic_pre_ok(const mdp_handle* h, int p, int k) {
+  const Topo& T = h->L.topo;
+  return h->critic_pre && !h->general_grads && grads_r_ok(T, p) && grads_r_ok(T, k) && !T.ag[k].local_q;
+}
+
 // strict data-parallel update of one agent (maddpg.py:188-194 order):
 // critic grads -> reduce -> all-reduce -> clip + Adam (x 1/G); then the actor
-int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out) {
+int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out, int post_prev, int pre_next,
+                 const int32_t* pre_idx) {
   const float scale = 1.0f / (float)h->dp_world;
   const bool pre = actor_pre_ok(h, agent);
   int rc;
   if (h->p2p) {  // the exchange lives inside the optimizer launch: same 4 launches as one GPU
-    if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre))) return rc;
+    if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre, nullptr, post_prev))) return rc;
     if ((rc = do_reduce_apply(h, agent, 1))) return rc;
-    if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre))) return rc;
+    if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre, pre_next, pre_idx))) return rc;
     return do_reduce_apply(h, agent, 0);
   }
-  if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre, nullptr, post_prev))) return rc;
   if ((rc = do_reduce(h, agent, 1))) return rc;
   if ((rc = dp_allreduce(h, agent, 1))) return rc;
   if ((rc = do_apply(h, agent, 1, false, scale))) return rc;
-  if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre))) return rc;
+  if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre, pre_next, pre_idx))) return rc;
   if ((rc = do_reduce(h, agent, 0))) return rc;
   if ((rc = dp_allreduce(h, agent, 0))) return rc;
   return do_apply(h, agent, 0, false, scale);
 }
 
 // pf_out: the critic kernel also draws the next round's indices there (fast path only)
+// post_prev >= 0: this critic step finishes the work that agent post_prev's
+// actor launch started (critic_post); pre_next >= 0: this actor launch starts
+// agent pre_next's next critic step on indices pre_idx (critic_pre)
 int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act,
-              int32_t* pf_out = nullptr) {
-  if ((h->comm || h->p2p) && !u_tgt && !u_act) return do_update_dp(h, agent, idx, pf_out);
+              int32_t* pf_out = nullptr, int post_prev = -1, int pre_next = -1, const int32_t* pre_idx = nullptr) {
+  if ((h->comm || h->p2p) && !u_tgt && !u_act)
+    return do_update_dp(h, agent, idx, pf_out, post_prev, pre_next, pre_idx);
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
   const bool pre = actor_pre_ok(h, agent);
-  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev))) return rc;
   if (fused) {
     if ((rc = do_reduce_apply(h, agent, 1))) return rc;
   } else {
     if ((rc = do_reduce(h, agent, 1))) return rc;
     if ((rc = do_apply(h, agent, 1, false, 1.0f))) return rc;
   }
-  if ((rc = do_actor_grad(h, agent, idx, u_act, false, pre))) return rc;
+  if ((rc = do_actor_grad(h, agent, idx, u_act, false, pre, pre_next, pre_idx))) return rc;
   if (fused) {
     if ((rc = do_reduce_apply(h, agent, 0))) return rc;
   } else {
@@ -851,6 +881,8 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
     CriticArgs a;
     a.apre = nullptr;
     a.u_act = nullptr;
+    a.cpre = nullptr;
+    a.cpre_prev = -1;
     a.pf_ctl = h->ctl;
     a.pf_out = pf_out;
     a.pf_count = pf_out ? n * h->cfg.batch_size : 0;
@@ -879,6 +911,10 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
   {
     ActorArgs a;
     a.apre = nullptr;
+    a.cpre = nullptr;
+    a.cpre_agent = -1;
+    a.cpre_idx = nullptr;
+    a.target = h->target;
     a.topo = h->L.topo;
     a.agent = 0;
     a.B = h->cfg.batch_size;
@@ -1009,6 +1045,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->rollout_draw = !(rd && rd[0] == '0');
     const char* ap = getenv("MDP_ACTOR_PRE");
     h->actor_pre = !(ap && ap[0] == '0');
+    const char* cp = getenv("MDP_CRITIC_PRE");
+    h->critic_pre = !(cp && cp[0] == '0');
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
@@ -1076,6 +1114,7 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->ra_ctr = (uint32_t*)p;
     h->ra_part = (uint64_t*)(p + (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128);
     h->apre = (float*)(p + mdp_ra_sync_bytes());
+    h->cpre = h->apre + (int64_t)nwg * 16 * MDP_APRE_W;
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
   std::vector<float> beta(8 * cfg->n_agents);
@@ -1353,11 +1392,34 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
   return do_update(h, agent, idx, u_tgt_dev, u_act_dev);
 }
 
-static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nullptr) {
+// One strict round.  Agent i's critic step is split around agent i-1's update
+// when critic_pre_ok: its independent part rides in i-1's actor launch.
+// carry_in: the previous round's last actor launch already did agent 0's part
+// (rounds of one training step, same replay contents); next_idx: the next
+// round's indices, if drawn by now (the prefetch in agent 0's critic launch),
+// lets this round's last actor launch do the next round's agent-0 part.
+// Returns in *carry_out whether it did.
+static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nullptr, bool carry_in = false,
+                         const int32_t* next_idx = nullptr, bool* carry_out = nullptr) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
+  if (carry_out) *carry_out = false;
   if (h->update_mode == 1) return do_round_tp(h, idx, nullptr, nullptr, pf_out);
   int rc = 0;
-  for (int i = 0; i < n && !rc; ++i) rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, i == 0 ? pf_out : nullptr);
+  for (int i = 0; i < n && !rc; ++i) {
+    const int post_prev = i > 0 ? (critic_pre_ok(h, i - 1, i) ? i - 1 : -1) : (carry_in ? n - 1 : -1);
+    int pre_next = -1;
+    const int32_t* pre_idx = nullptr;
+    if (i + 1 < n && critic_pre_ok(h, i, i + 1)) {
+      pre_next = i + 1;
+      pre_idx = idx + (int64_t)(i + 1) * B;
+    } else if (i + 1 == n && next_idx && critic_pre_ok(h, n - 1, 0)) {
+      pre_next = 0;
+      pre_idx = next_idx;
+      if (carry_out) *carry_out = true;
+    }
+    rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, i == 0 ? pf_out : nullptr, post_prev, pre_next,
+                   pre_idx);
+  }
   return rc;
 }
 
@@ -1741,9 +1803,11 @@ static int step_launches(mdp_handle* h, int rounds) {
   if (rc || rounds == 0) return rc;
   const bool pf = prefetch_ok(h);
   if (!in_rollout && (rc = launch_make_index(h, nb, slot[0]))) return rc;
+  bool carry = false;
   for (int r = 0; r < rounds && !rc; ++r) {
     const bool more = r + 1 < rounds;
-    rc = round_updates(h, slot[r & 1], (more && pf) ? slot[(r + 1) & 1] : nullptr);
+    int32_t* next = (more && pf) ? slot[(r + 1) & 1] : nullptr;  // drawn in agent 0's critic launch
+    rc = round_updates(h, slot[r & 1], next, carry, next, &carry);
     if (!rc && more && !pf) rc = launch_make_index(h, nb, slot[(r + 1) & 1]);
   }
   return rc;

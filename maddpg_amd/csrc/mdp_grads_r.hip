@@ -207,6 +207,154 @@ __device__ __forceinline__ void actor_pre_tile(const CriticArgs& a, float* lds, 
   for (int q = threadIdx.x; q < MDP_R * MDP_APRE_W / 4; q += blockDim.x)
     *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(apre_lds(q, h1a, h2a, lg, av));
 }
+// float4 q of a row block [16][MDP_CPRE_W] <-> its LDS home (h1c | h2c | tacc | q + pad)
+__device__ __forceinline__ float* cpre_lds(int q, float* h1c, float* h2c, float* tacc, float* qv4) {
+  const int row = q / (MDP_CPRE_W / 4), c = 4 * (q - row * (MDP_CPRE_W / 4));
+  return c < 64 ? h1c + row * LH + c : c < 128 ? h2c + row * LH + c - 64 : c < 192 ? tacc + row * LH + c - 128
+                                                                                    : qv4 + row * 4;
+}
+
+// extra workgroup of k_actor_grad_r (agent p's actor step): the next critic
+// step's (agent k, MADDPG critic) work that p's coming update does not touch,
+// for row tile bx -- target actors j != p with their Gumbel samples (maddpg.py:
+// 183), the critic forward q(o, a) (:85-88), and the target critic's layer-1
+// accumulator over obs' and a~_j, j != p (:104; p's weight rows read as zero)
+// -- into cpre.  Roles as k_critic_grad_r: waves 0..2 target actors, wave 3
+// the critic, waves 4..7 gather and one target-critic column tile each.
+__device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, int* rows_ready, int bx) {
+  const Topo& T = a.topo;
+  const int k = a.cpre_agent, p = a.agent;
+  const ADesc& ag = T.ag[k];
+  const NDesc& nd = ag.critic;
+  const int na = T.n;
+  const int ldr = lds_ld(T.row_stride);
+  const int kb = MDP_ACT_DIM * na, ldA = lds_ld(kb);
+  const int ka_t = T.sum_obs, xo_t = T.ag[0].nobs_off, ka_c = ag.cin;
+  LdsCarve cv(lds);
+  float* rowbuf = cv.take(MDP_R * ldr);
+  float* xa = cv.take(MDP_R * ldA);
+  float* lg = cv.take(3 * MDP_R * 8);
+  float* h1a = cv.take(3 * MDP_R * LH);
+  float* h2a = cv.take(3 * MDP_R * LH);
+  float* h1c = cv.take(MDP_R * LH);
+  float* h2c = cv.take(MDP_R * LH);
+  float* tacc = cv.take(MDP_R * LH);
+  float* qv4 = cv.take(MDP_R * 4);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int r0 = bx * MDP_R, nvalid = min(MDP_R, a.B - r0);
+  const uint32_t ctr = a.ctl->upd_ctr + 1u;  // critic k runs after p's actor step advanced the counter
+  const float* Pc = a.theta;
+  const float* Pt = a.target;
+  if (threadIdx.x == 0) *rows_ready = 0;
+  __syncthreads();
+  if (wave < 3) {
+    if (wave < na && wave != p) {
+      const int j = wave;
+      const ADesc& aj = T.ag[j];
+      const NDesc& an = aj.actor;
+      f32x4 w1[16], w2[16];
+      float w3[16];
+      rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
+      rf_load<16>(w2, Pt + an.t[2].off, RH, 0, 0);
+      rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
+      const f32x4 b1 = ld4(Pt + an.t[1].off + 4 * r), b2 = ld4(Pt + an.t[3].off + 4 * r);
+      const float b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
+      float gn[MDP_ACT_DIM];
+      {
+        float u[MDP_ACT_DIM];
+        uniforms5(a.seed, (uint32_t)((k << 8) | (j + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
+        gumbel_noise5(u, gn);
+      }
+      lds_wait(rows_ready, 4);
+      float* h1 = h1a + wave * MDP_R * LH;
+      float* h2 = h2a + wave * MDP_R * LH;
+      float* lgj = lg + wave * MDP_R * 8;
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<16>(acc, rowbuf + aj.nobs_off, ldr, aj.obs_dim, w1);
+        rf_store<true>(acc, b1, h1, LH);
+      }
+      wave_sync();
+      {
+        f32x4 acc[4];
+        rf_zero(acc);
+        rf_acc<16>(acc, h1, LH, RH, w2);
+        rf_store<true>(acc, b2, h2, LH);
+      }
+      wave_sync();
+      {
+        const f32x4 acc = rh_acc(h2, LH, w3);
+        if (r < MDP_ACT_DIM) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lgj[(kq * 4 + i) * 8 + r] = acc[i] + b3;
+        }
+      }
+      wave_sync();
+      if (lane < MDP_R) {
+        float act[MDP_ACT_DIM];
+        gumbel_softmax5_pre(lgj + lane * 8, gn, act);
+        for (int q = 0; q < MDP_ACT_DIM; ++q) xa[lane * ldA + MDP_ACT_DIM * j + q] = act[q];
+      }
+    } else if (wave == p && lane < MDP_R) {  // p's slot: zero weights meet zeros (not stale LDS, e.g. NaN)
+      for (int q = 0; q < MDP_ACT_DIM; ++q) xa[lane * ldA + MDP_ACT_DIM * p + q] = 0.f;
+    }
+    __syncthreads();  // B2: a~_j (j != p) ready
+  } else if (wave == 3) {
+    f32x4 w1[20], w2[16];
+    float w3[16];
+    rf_load<20>(w1, Pc + nd.t[0].off, ka_c, 0, 0);
+    rf_load<16>(w2, Pc + nd.t[2].off, RH, 0, 0);
+    rq_load(w3, Pc + nd.t[4].off);
+    const f32x4 b1 = ld4(Pc + nd.t[1].off + 4 * r), b2 = ld4(Pc + nd.t[3].off + 4 * r);
+    const float b3 = Pc[nd.t[5].off];
+    lds_wait(rows_ready, 4);
+    {
+      f32x4 acc[4];
+      rf_zero(acc);
+      rf_acc<20>(acc, rowbuf, ldr, ka_c, w1);
+      rf_store<true>(acc, b1, h1c, LH);
+    }
+    wave_sync();
+    {
+      f32x4 acc[4];
+      rf_zero(acc);
+      rf_acc<16>(acc, h1c, LH, RH, w2);
+      rf_store<true>(acc, b2, h2c, LH);
+    }
+    wave_sync();
+    const float q = rq_head(h2c, LH, w3) + b3;
+    if ((lane & 3) == 0) {
+      qv4[(lane >> 2) * 4] = q;
+      qv4[(lane >> 2) * 4 + 1] = qv4[(lane >> 2) * 4 + 2] = qv4[(lane >> 2) * 4 + 3] = 0.f;
+    }
+    __syncthreads();  // B2
+  } else {
+    const int tt = wave - 4, col = 16 * tt + r;
+    gather_rows16_part(a.replay, T.row_stride, a.cpre_idx, r0, nvalid, rowbuf, ldr, 256, 256);
+    lds_signal(rows_ready);
+    float wa[16], wb[5];
+    rt_load<16>(wa, Pt + nd.t[0].off, RH, col, ka_t);
+    rt_load<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, kb);
+#pragma unroll
+    for (int s2 = 0; s2 < 5; ++s2) {  // p's target-action rows: added by the critic step itself
+      const int kk = 4 * s2 + kq;
+      if (kk >= MDP_ACT_DIM * p && kk < MDP_ACT_DIM * (p + 1)) wb[s2] = 0.f;
+    }
+    lds_wait(rows_ready, 4);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
+    __syncthreads();  // B2: a~ ready
+    rt_acc<5>(acc, xa, ldA, kb, wb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tacc[(kq * 4 + i) * LH + col] = acc[i];
+  }
+  __syncthreads();  // B3
+  float* dst = a.cpre + (int64_t)r0 * MDP_CPRE_W;
+  for (int q = threadIdx.x; q < MDP_R * MDP_CPRE_W / 4; q += blockDim.x)
+    *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(cpre_lds(q, h1c, h2c, tacc, qv4));
+}
 }  // namespace
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
@@ -268,6 +416,9 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)agent : 0u);
   const float* Pc = a.theta;
   const float* Pt = a.target;
+  // critic_post: target actor pprev is the only one left (see CriticArgs::cpre)
+  const bool post = a.cpre != nullptr;
+  const int pprev = a.cpre_prev;
   const int64_t ao = a.multi > 1 ? (int64_t)agent : 0;  // per-agent output blocks (throughput mode)
   float* slab = a.slab + ao * a.slab_agent_stride + (int64_t)bx * a.slab_stride - nd.off;
   double* slab_stat = a.slab_stat + ao * (int64_t)((a.B + MDP_R - 1) / MDP_R) * 8;
@@ -278,9 +429,9 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 
   if (wave < 4) {
     f32x4 wt[4];  // W2^T tile of the critic for dh1 (loaded once this wave's forward weights are dead)
-    if (wave < na) {
+    if (post ? wave == 0 : wave < na) {
       // ---------------- target actor j on obs'_j, Gumbel-softmax target action (maddpg.py:183)
-      const int j = lq ? agent : wave;
+      const int j = post ? pprev : (lq ? agent : wave);
       const ADesc& aj = T.ag[j];
       const NDesc& an = aj.actor;
 #ifdef MDP_STAMPS
@@ -363,6 +514,27 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       MDP_CLK(44);
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       __syncthreads();  // B2
+    } else if (wave == 3 && post) {
+      // ---------------- critic_post: h1c, h2c, q of the forward done in the previous actor launch
+      const float* src = a.cpre + (int64_t)r0 * MDP_CPRE_W;
+      constexpr int Q = MDP_CPRE_W / 4, IT = (MDP_R * Q + 63) / 64;
+      f32x4 v[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int q = min(lane + 64 * it, MDP_R * Q - 1);
+        v[it] = ld4(src + 4 * q);
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int q = lane + 64 * it, row = q / Q, c = 4 * (q - row * Q);
+        if (q < MDP_R * Q) {
+          if (c < 64) *reinterpret_cast<f32x4*>(h1c + row * LH + c) = v[it];
+          else if (c < 128) *reinterpret_cast<f32x4*>(h2c + row * LH + c - 64) = v[it];
+          else if (c == 192) qv[row] = v[it][0];
+        }
+      }
+      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      __syncthreads();  // B2
     } else if (wave == 3) {
       // ---------------- online critic forward q(o, a) (maddpg.py:85-88, 104)
       f32x4 w1[20], w1b[2], w2[16];
@@ -417,19 +589,27 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     }
 #endif
     float wa[16], wb[5], w2[16], w3[16];
-    rt_load<16>(wa, Pt + nd.t[0].off, RH, col, ka_t);
-    rt_load<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, kb);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (post) {  // the accumulator over obs' and a~_j (j != pprev) from cpre; W1 rows of a~_pprev
+      rt_load<5>(wb, Pt + nd.t[0].off + (ka_t + MDP_ACT_DIM * pprev) * RH, RH, col, MDP_ACT_DIM);
+      const float* src = a.cpre + (int64_t)r0 * MDP_CPRE_W + 128 + col;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = src[(kq * 4 + i) * MDP_CPRE_W];
+    } else {
+      rt_load<16>(wa, Pt + nd.t[0].off, RH, col, ka_t);
+      rt_load<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, kb);
+    }
     rt_load<16>(w2, Pt + nd.t[2].off, RH, col, RH);
     const float b1 = Pt[nd.t[1].off + col], b2 = Pt[nd.t[3].off + col];
     if (tt == 0) rq_load(w3, Pt + nd.t[4].off);
     const float b3 = Pt[nd.t[5].off];
     const float w3c = Pc[nd.t[4].off + lane];  // d2 = dq * W3 of the online critic
     lds_wait(&rows_ready, 4);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
+    if (!post) rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
     __syncthreads();  // B2: a~ ready
     if (tt == 0) MDP_STAMPW(4);
-    rt_acc<5>(acc, xa, ldA, kb, wb);
+    if (post) rt_acc<5>(acc, xa + MDP_ACT_DIM * pprev, ldA, MDP_ACT_DIM, wb);
+    else rt_acc<5>(acc, xa, ldA, kb, wb);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h1t[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b1, 0.f);
     __syncthreads();  // B3
@@ -506,6 +686,13 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;
   int agent = a.agent, bx = blockIdx.x;
+  if (a.cpre) {  // workgroups [B/16, 2 B/16): the next critic step's independent work (strict mode)
+    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    if (bx >= nwg) {
+      critic_pre_tile(a, lds, &rows_ready, bx - nwg);
+      return;
+    }
+  }
   if (a.multi > 1) {  // throughput mode: every agent's actor step in this launch
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
     agent = bx / nwg;
@@ -730,7 +917,8 @@ hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStrea
 }
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s) {
   static bool attr = false;
-  return launch_r(k_actor_grad_r, a, lds_bytes, s, attr);
+  // grid: actor row tiles | the next critic step's row tiles (a.cpre)
+  return launch_r(k_actor_grad_r, a, lds_bytes, s, attr, a.cpre ? (a.B + MDP_R - 1) / MDP_R : 0);
 }
 
 #ifdef MDP_STAMPS

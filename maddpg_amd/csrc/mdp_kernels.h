@@ -38,7 +38,20 @@ struct CriticArgs {
   // u_act: injected uniforms of that sample or null (0: no extra workgroups)
   float* apre;
   const float* u_act;
+  // critic_post mode (k_critic_grad_r): the work of this critic step that does
+  // not depend on the previous agent's update (target actors j != cpre_prev,
+  // the critic forward, the target critic's layer-1 accumulator over obs' and
+  // those target actions) was done by extra workgroups of that agent's actor
+  // launch into cpre [B][MDP_CPRE_W]; only target actor cpre_prev (Polyak-
+  // updated since) and the rest of the step remain (null: the full step)
+  const float* cpre;
+  int cpre_prev;
 };
+
+// precomputed critic-step work of one batch row (k_actor_grad_r's extra
+// workgroups -> k_critic_grad_r in critic_post mode):
+//   h1 [64] | h2 [64] (critic forward) | target-critic L1 accumulator [64] | q | pad 3
+#define MDP_CPRE_W 196
 
 // precomputed actor forward of one batch row (k_critic_grad_r's extra
 // workgroups -> k_actor_grad_r): h1 [64] | h2 [64] | logits [8] | sample [8]
@@ -61,6 +74,12 @@ struct ActorArgs {
   int multi;                  // throughput mode, as CriticArgs
   int64_t slab_agent_stride;
   const float* apre;          // k_actor_grad_r: the forward precomputed by the critic launch, or null
+  // k_actor_grad_r: B/16 extra workgroups run the NEXT critic step's
+  // independent work (agent cpre_agent, indices cpre_idx) into cpre (null: none)
+  float* cpre;
+  int cpre_agent;
+  const int32_t* cpre_idx;
+  const float* target;        // target nets (the critic_pre role's target actors / critic)
 };
 
 struct ReduceArgs {
@@ -236,6 +255,11 @@ inline int lds_critic_r_bytes(const Topo& t, int agent) {
 inline int lds_actor_r_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, LD = 65;
   return 4 * (mdp_r4(R * ldr) + 4 * R * 8 + R + 3 * R * LH + 4 * mdp_r4(R * LD) + 2 * 64 * 16 + 4 * R + 4 * 5 * 64);
+}
+// critic_pre role of k_actor_grad_r (mirrors critic_pre_tile's carve)
+inline int lds_critic_pre_bytes(const Topo& t) {
+  const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, ldA = mdp_ld(5 * t.n);
+  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldA) + 3 * R * 8 + 6 * R * LH + 3 * R * LH + 4 * R);
 }
 // the fast kernels hold every weight of a wave in registers: H = 64, at most 3
 // target actors, actor inputs <= 64, critic inputs <= 80, target-critic action part <= 20
