@@ -818,6 +818,20 @@ __device__ __forceinline__ void rt_load(float (&w)[KS], const float* __restrict_
     w[s] = k < K ? v : 0.f;
   }
 }
+// rt_load for a runtime K <= 4 KS: only the k-steps below K issue loads
+template <int KS>
+__device__ __forceinline__ void rt_load_k(float (&w)[KS], const float* __restrict__ W, int ldw, int col, int K) {
+  const int kq = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    w[s] = 0.f;
+    if (4 * s < K) {  // wave-uniform
+      const int k = 4 * s + kq;
+      const float v = W[min(k, K - 1) * ldw + col];
+      w[s] = k < K ? v : 0.f;
+    }
+  }
+}
 template <int KS>
 __device__ __forceinline__ void rt_acc(f32x4& acc, const float* X, int ldx, int K, const float (&w)[KS]) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;

@@ -207,12 +207,16 @@ __device__ __forceinline__ void actor_pre_tile(const CriticArgs& a, float* lds, 
   for (int q = threadIdx.x; q < MDP_R * MDP_APRE_W / 4; q += blockDim.x)
     *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(apre_lds(q, h1a, h2a, lg, av));
 }
-// float4 q of a row block [16][MDP_CPRE_W] <-> its LDS home (h1c | h2c | tacc | q + pad)
-__device__ __forceinline__ float* cpre_lds(int q, float* h1c, float* h2c, float* tacc, float* qv4) {
+// float4 q of a row block [16][MDP_CPRE_W] <-> its LDS home (h1c | h2c | tacc | q + pad | a~ [16])
+__device__ __forceinline__ float* cpre_lds(int q, float* h1c, float* h2c, float* tacc, float* qv4, float* xa16) {
   const int row = q / (MDP_CPRE_W / 4), c = 4 * (q - row * (MDP_CPRE_W / 4));
   return c < 64 ? h1c + row * LH + c : c < 128 ? h2c + row * LH + c - 64 : c < 192 ? tacc + row * LH + c - 128
-                                                                                    : qv4 + row * 4;
+                                                                         : c < 196 ? qv4 + row * 4
+                                                                                   : xa16 + row * 16 + c - 196;
 }
+// first MFMA k-step (of 4 inputs) of the target critic's a~ part that holds a
+// target action of agent p (columns 5 p .. 5 p + 4)
+__device__ __forceinline__ int cpre_split(int p) { return (MDP_ACT_DIM * p) / 4; }
 
 // extra workgroup of k_actor_grad_r (agent p's actor step): the next critic
 // step's (agent k, MADDPG critic) work that p's coming update does not touch,
@@ -240,6 +244,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
   float* h2c = cv.take(MDP_R * LH);
   float* tacc = cv.take(MDP_R * LH);
   float* qv4 = cv.take(MDP_R * 4);
+  float* xa16 = cv.take(MDP_R * 16);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int r0 = bx * MDP_R, nvalid = min(MDP_R, a.B - r0);
@@ -334,26 +339,26 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
     const int tt = wave - 4, col = 16 * tt + r;
     gather_rows16_part(a.replay, T.row_stride, a.cpre_idx, r0, nvalid, rowbuf, ldr, 256, 256);
     lds_signal(rows_ready);
+    // the k-steps of the a~ part before p's first target action (rows 0 .. 4 ks - 1)
+    const int ks = cpre_split(p);
     float wa[16], wb[5];
     rt_load<16>(wa, Pt + nd.t[0].off, RH, col, ka_t);
-    rt_load<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, kb);
-#pragma unroll
-    for (int s2 = 0; s2 < 5; ++s2) {  // p's target-action rows: added by the critic step itself
-      const int kk = 4 * s2 + kq;
-      if (kk >= MDP_ACT_DIM * p && kk < MDP_ACT_DIM * (p + 1)) wb[s2] = 0.f;
-    }
+    rt_load_k<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, 4 * ks);
     lds_wait(rows_ready, 4);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
     __syncthreads();  // B2: a~ ready
-    rt_acc<5>(acc, xa, ldA, kb, wb);
+    if (ks > 0) rt_acc<5>(acc, xa, ldA, 4 * ks, wb);
 #pragma unroll
     for (int i = 0; i < 4; ++i) tacc[(kq * 4 + i) * LH + col] = acc[i];
+    if (tt == 0 && lane < MDP_R) {  // every a~_j (p's slot zero: the critic step writes it)
+      for (int c = 0; c < 16; ++c) xa16[lane * 16 + c] = c < kb ? xa[lane * ldA + c] : 0.f;
+    }
   }
   __syncthreads();  // B3
   float* dst = a.cpre + (int64_t)r0 * MDP_CPRE_W;
   for (int q = threadIdx.x; q < MDP_R * MDP_CPRE_W / 4; q += blockDim.x)
-    *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(cpre_lds(q, h1c, h2c, tacc, qv4));
+    *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(cpre_lds(q, h1c, h2c, tacc, qv4, xa16));
 }
 }  // namespace
 
@@ -366,6 +371,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   }
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;  // gather waves done (LDS hand-off, replaces a barrier)
+  __shared__ int post_sync[2];  // critic_post: target-actor L1, L2 tiles of waves 0..3 done
   int agent = a.agent, bx = blockIdx.x;
   if (a.apre) {  // workgroups [B/16, 2 B/16): the actor step's forward (strict mode only)
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
@@ -425,13 +431,102 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   double* y_out = a.y_out + ao * a.B;
   MDP_STAMP(0);
   if (threadIdx.x == 0) rows_ready = 0;
+  if (threadIdx.x < 2) post_sync[threadIdx.x] = 0;
   __syncthreads();  // B0 (nothing in flight yet)
 
   if (wave < 4) {
     f32x4 wt[4];  // W2^T tile of the critic for dh1 (loaded once this wave's forward weights are dead)
-    if (post ? wave == 0 : wave < na) {
+    if (post) {
+      // ---------------- critic_post: target actor pprev (Polyak-updated since the
+      // critic_pre) over waves 0..3, one 16-column tile of L1 and L2 each, the
+      // head as split-K partials over the tiles; wave 3 also loads h1c, h2c, q
+      const ADesc& aj = T.ag[pprev];
+      const NDesc& an = aj.actor;
+      const int col = 16 * wave + r;
+      if (wave > 0) {
+        // the cpre block, issued first: wave 1 h1c, wave 2 h2c, wave 3 q and the a~ (not pprev's)
+        const float* src = a.cpre + (int64_t)r0 * MDP_CPRE_W;
+        const int c0 = wave == 1 ? 0 : (wave == 2 ? 64 : 192), nc4 = wave == 3 ? 5 : 16;
+        f32x4 v[4];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int q = min(lane + 64 * it, MDP_R * nc4 - 1), row = q / nc4;
+          v[it] = ld4(src + (int64_t)row * MDP_CPRE_W + c0 + 4 * (q - row * nc4));
+        }
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int q = lane + 64 * it, row = q / nc4, c = c0 + 4 * (q - row * nc4);
+          if (q < MDP_R * nc4) {
+            if (c < 64) *reinterpret_cast<f32x4*>(h1c + row * LH + c) = v[it];
+            else if (c < 128) *reinterpret_cast<f32x4*>(h2c + row * LH + c - 64) = v[it];
+            else if (c == 192) qv[row] = v[it][0];
+            else {  // the stored target actions (not pprev's slot: wave 0 writes it)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int cc = c - 196 + e;
+                if (cc < kb && (cc < MDP_ACT_DIM * pprev || cc >= MDP_ACT_DIM * (pprev + 1)))
+                  xa[row * ldA + cc] = v[it][e];
+              }
+            }
+          }
+        }
+      }
+      float w1t[16], w2t[16], w3[16];
+      rt_load_k<16>(w1t, Pt + an.t[0].off, RH, col, aj.obs_dim);
+      rt_load<16>(w2t, Pt + an.t[2].off, RH, col, RH);
+      const float b1 = Pt[an.t[1].off + col], b2 = Pt[an.t[3].off + col];
+      float gn[MDP_ACT_DIM], b3 = 0.f;
+      if (wave == 0) {  // the head (one MFMA chain, as the unsplit step) and the Gumbel noise
+        rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
+        b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
+        float u[MDP_ACT_DIM];
+        uniforms5(a.seed, (uint32_t)((agent << 8) | (pprev + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
+        gumbel_noise5(u, gn);
+      }
+      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      float* h1 = h1a;
+      float* h2 = h2a;
+      if (wave == 0) MDP_STAMPW(48);
+      if (wave == 3) MDP_STAMPW(54);
+      lds_wait(&rows_ready, 4);
+      if (wave == 0) MDP_STAMPW(49);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      rt_acc<16>(acc, rowbuf + aj.nobs_off, ldr, aj.obs_dim, w1t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h1[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b1, 0.f);
+      lds_signal(&post_sync[0]);
+      lds_wait(&post_sync[0], 4);
+      acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      rt_acc<16>(acc, h1, LH, RH, w2t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h2[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b2, 0.f);
+      lds_signal(&post_sync[1]);
+      if (wave == 0) MDP_STAMPW(50);
+      if (wave == 3) MDP_STAMPW(55);
+      if (wave == 0) {
+        lds_wait(&post_sync[1], 4);
+        MDP_STAMPW(51);
+        float* lgj = lg;
+        {
+          const f32x4 hacc = rh_acc(h2, LH, w3);
+          if (r < MDP_ACT_DIM) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lgj[(kq * 4 + i) * 8 + r] = hacc[i] + b3;
+          }
+        }
+        wave_sync();
+        if (lane < MDP_R) {  // distributions.py:264-266
+          float act[MDP_ACT_DIM];
+          gumbel_softmax5_pre(lgj + lane * 8, gn, act);
+          for (int c = 0; c < MDP_ACT_DIM; ++c) xa[lane * ldA + MDP_ACT_DIM * pprev + c] = act[c];
+        }
+        MDP_STAMPW(52);
+      }
+      __syncthreads();  // B2
+      if (wave == 0) MDP_STAMPW(53);
+    } else if (wave < na) {
       // ---------------- target actor j on obs'_j, Gumbel-softmax target action (maddpg.py:183)
-      const int j = post ? pprev : (lq ? agent : wave);
+      const int j = lq ? agent : wave;
       const ADesc& aj = T.ag[j];
       const NDesc& an = aj.actor;
 #ifdef MDP_STAMPS
@@ -514,27 +609,6 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       MDP_CLK(44);
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       __syncthreads();  // B2
-    } else if (wave == 3 && post) {
-      // ---------------- critic_post: h1c, h2c, q of the forward done in the previous actor launch
-      const float* src = a.cpre + (int64_t)r0 * MDP_CPRE_W;
-      constexpr int Q = MDP_CPRE_W / 4, IT = (MDP_R * Q + 63) / 64;
-      f32x4 v[IT];
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int q = min(lane + 64 * it, MDP_R * Q - 1);
-        v[it] = ld4(src + 4 * q);
-      }
-#pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int q = lane + 64 * it, row = q / Q, c = 4 * (q - row * Q);
-        if (q < MDP_R * Q) {
-          if (c < 64) *reinterpret_cast<f32x4*>(h1c + row * LH + c) = v[it];
-          else if (c < 128) *reinterpret_cast<f32x4*>(h2c + row * LH + c - 64) = v[it];
-          else if (c == 192) qv[row] = v[it][0];
-        }
-      }
-      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
-      __syncthreads();  // B2
     } else if (wave == 3) {
       // ---------------- online critic forward q(o, a) (maddpg.py:85-88, 104)
       f32x4 w1[20], w1b[2], w2[16];
@@ -590,8 +664,9 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 #endif
     float wa[16], wb[5], w2[16], w3[16];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (post) {  // the accumulator over obs' and a~_j (j != pprev) from cpre; W1 rows of a~_pprev
-      rt_load<5>(wb, Pt + nd.t[0].off + (ka_t + MDP_ACT_DIM * pprev) * RH, RH, col, MDP_ACT_DIM);
+    const int ks = post ? cpre_split(pprev) : 0;
+    if (post) {  // the accumulator up to k-step ks from cpre; W1 rows of the a~ k-steps from ks on
+      rt_load_k<5>(wb, Pt + nd.t[0].off + (ka_t + 4 * ks) * RH, RH, col, kb - 4 * ks);
       const float* src = a.cpre + (int64_t)r0 * MDP_CPRE_W + 128 + col;
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[i] = src[(kq * 4 + i) * MDP_CPRE_W];
@@ -608,7 +683,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     if (!post) rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
     __syncthreads();  // B2: a~ ready
     if (tt == 0) MDP_STAMPW(4);
-    if (post) rt_acc<5>(acc, xa + MDP_ACT_DIM * pprev, ldA, MDP_ACT_DIM, wb);
+    if (post) rt_acc<5>(acc, xa + 4 * ks, ldA, kb - 4 * ks, wb);
     else rt_acc<5>(acc, xa, ldA, kb, wb);
 #pragma unroll
     for (int i = 0; i < 4; ++i) h1t[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b1, 0.f);

@@ -50,8 +50,12 @@ struct CriticArgs {
 
 // precomputed critic-step work of one batch row (k_actor_grad_r's extra
 // workgroups -> k_critic_grad_r in critic_post mode):
-//   h1 [64] | h2 [64] (critic forward) | target-critic L1 accumulator [64] | q | pad 3
-#define MDP_CPRE_W 196
+//   h1 [64] | h2 [64] (critic forward) | target-critic L1 accumulator [64] | q | pad 3 | a~ [16]
+// The accumulator stops at the first MFMA k-step holding a target action of
+// the previous agent; critic_post resumes the chain there with every a~ (the
+// stored ones + the fresh one), so the result is bit-identical to the
+// unsplit critic step
+#define MDP_CPRE_W 212
 
 // precomputed actor forward of one batch row (k_critic_grad_r's extra
 // workgroups -> k_actor_grad_r): h1 [64] | h2 [64] | logits [8] | sample [8]
@@ -259,7 +263,7 @@ inline int lds_actor_r_bytes(const Topo& t) {
 // critic_pre role of k_actor_grad_r (mirrors critic_pre_tile's carve)
 inline int lds_critic_pre_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, ldA = mdp_ld(5 * t.n);
-  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldA) + 3 * R * 8 + 6 * R * LH + 3 * R * LH + 4 * R);
+  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldA) + 3 * R * 8 + 6 * R * LH + 3 * R * LH + 4 * R + 16 * R);
 }
 // the fast kernels hold every weight of a wave in registers: H = 64, at most 3
 // target actors, actor inputs <= 64, critic inputs <= 80, target-critic action part <= 20

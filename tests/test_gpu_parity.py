@@ -642,3 +642,42 @@ def test_env_benchmark_data_parity(name, n, na):
     s1 = Engine([4], batch_size=16, capacity=100, num_envs=4, scenario="simple")
     with pytest.raises(Exception, match="benchmark_data"):
         s1.env_step_bench()
+
+
+@pytest.mark.parametrize("dims,local_q", [([18, 18, 18], None), ([8, 10, 10], [True, False, False]), ([4], None)])
+def test_split_steps_bit_identical(monkeypatch, dims, local_q):
+    """The actor step's forward computed in the critic launch (actor_pre) and
+    the critic step split around the previous agent's update (critic_pre ->
+    critic_post, also across rounds of one training step) are scheduling
+    choices: the same MFMA chains in the same order.  Three rounds with both on
+    (update_round), with both off (MDP_ACTOR_PRE=0 MDP_CRITIC_PRE=0), and
+    agent by agent through mdp_update (no cross-agent split) must agree bit for bit."""
+    B, L = 256, 3000
+    c = synthetic_trainer_case(dims, B, L, seed=91, local_q=local_q)
+    n = len(dims)
+
+    def run(mode):
+        eng = Engine(dims, c["local_q"], batch_size=B, capacity=L)
+        eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+        eng.init_params(4)
+        eng.seed_py_random(17)
+        for _ in range(3):
+            if mode == "agents":
+                for i in range(n):
+                    eng.update(i)
+            else:
+                eng.update_round()
+        eng.synchronize()
+        return eng
+
+    on, agents = run("round"), run("agents")
+    monkeypatch.setenv("MDP_ACTOR_PRE", "0")
+    monkeypatch.setenv("MDP_CRITIC_PRE", "0")
+    off = run("round")
+    for i in range(n):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_actor", "v_critic"):
+            a, b, d = on.get_params(i, w), off.get_params(i, w), agents.get_params(i, w)
+            for k in a:
+                np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k} split vs unsplit")
+                np.testing.assert_array_equal(a[k], d[k], err_msg=f"{i} {w} {k} round vs per-agent")
+        np.testing.assert_array_equal(on.stats(i), off.stats(i))

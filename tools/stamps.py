@@ -72,6 +72,11 @@ for lo, hi in seq:
         print(f"{names.get(i, i):>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us  (t={(st[i] - st[lo]) * 10 / 1000:6.2f})")
         prev = st[i]
     print()
+if fast and st[48]:
+    # critic_post (the last critic launch of the round: agent n-1, split around agent n-2)
+    print("critic_post from start: w0 loads issued %.2f, rows %.2f, L1 tile %.2f, L2 tiles all %.2f, head+gumbel %.2f, "
+          "B2 %.2f | w3 cpre loaded %.2f, w3 L2 tile %.2f us" % tuple(
+              (st[i] - st[0]) * 10 / 1000 for i in (48, 49, 50, 51, 52, 53, 54, 55)))
 lib_ra = getattr(lib, "mdp_debug_stamps_ra", None)
 if lib_ra is not None:
     lib_ra.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
