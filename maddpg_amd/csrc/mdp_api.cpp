@@ -206,7 +206,7 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   // computes every agent's gradients in one launch; strict mode uses block 0)
   sz[MDP_R_SLAB] = (int64_t)n * (4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg +
                                   8 * (int64_t)c->batch_size) + 256 + 256 + mdp_ra_sync_bytes() +
-                   4 * (int64_t)L.nwg * 16 * (MDP_APRE_W + MDP_CPRE_W);  // precomputed actor / critic work
+                   4 * (int64_t)L.nwg * 16 * (MDP_APRE_W + MDP_CPRE_W + 2 * T.row_stride);  // precomputed work + rows
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
   for (int r = 0; r < MDP_R_COUNT; ++r) {
@@ -296,6 +296,8 @@ struct mdp_handle {
   // -> critic_post; fast kernels, strict order; MDP_CRITIC_PRE=0: off)
   float* cpre = nullptr;
   bool critic_pre = true;
+  float* apre_rows = nullptr;  // the replay rows those launches gathered (read contiguously by the step)
+  float* cpre_rows = nullptr;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
   // mdp_train_step graphs (rollout + k rounds), one per k
@@ -452,6 +454,8 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.apre = nullptr;
   a.u_act = u_act;
   a.cpre = nullptr;
+  a.cpre_rows = h->cpre_rows;
+  a.apre_rows = h->apre_rows;
   a.cpre_prev = post_prev;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
@@ -504,7 +508,9 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
                   bool apre = false, int pre_next = -1, const int32_t* pre_idx = nullptr) {
   ActorArgs a;
   a.apre = apre ? h->apre : nullptr;
+  a.apre_rows = h->apre_rows;
   a.cpre = nullptr;
+  a.cpre_rows = h->cpre_rows;
   a.cpre_agent = pre_next;
   a.cpre_idx = pre_idx;
   a.target = h->target;
@@ -880,8 +886,10 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
   {
     CriticArgs a;
     a.apre = nullptr;
+    a.apre_rows = nullptr;
     a.u_act = nullptr;
     a.cpre = nullptr;
+    a.cpre_rows = nullptr;
     a.cpre_prev = -1;
     a.pf_ctl = h->ctl;
     a.pf_out = pf_out;
@@ -911,7 +919,9 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
   {
     ActorArgs a;
     a.apre = nullptr;
+    a.apre_rows = nullptr;
     a.cpre = nullptr;
+    a.cpre_rows = nullptr;
     a.cpre_agent = -1;
     a.cpre_idx = nullptr;
     a.target = h->target;
@@ -1115,6 +1125,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->ra_part = (uint64_t*)(p + (int64_t)MDP_MAX_AGENTS * 2 * 8 * 128);
     h->apre = (float*)(p + mdp_ra_sync_bytes());
     h->cpre = h->apre + (int64_t)nwg * 16 * MDP_APRE_W;
+    h->apre_rows = h->cpre + (int64_t)nwg * 16 * MDP_CPRE_W;
+    h->cpre_rows = h->apre_rows + (int64_t)nwg * 16 * h->L.topo.row_stride;
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
   std::vector<float> beta(8 * cfg->n_agents);

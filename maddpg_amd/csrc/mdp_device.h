@@ -671,6 +671,31 @@ __device__ __forceinline__ void gather_rows16_part(const float* __restrict__ rep
   }
 }
 
+// the 16 rows of a contiguous [16][stride] block (stored by an earlier launch's
+// gather) into rowbuf, over the threads [t0, t0 + nt): one round trip, no index load
+__device__ __forceinline__ void load_rows16_part(const float* __restrict__ block, int stride, float* rowbuf, int ldr,
+                                                 int t0, int nt) {
+  const int v4 = stride >> 2;
+  for (int e = (int)threadIdx.x - t0; e < MDP_R * v4; e += nt) {
+    const int r = e / v4, c4 = e - r * v4;
+    const float4 v = *reinterpret_cast<const float4*>(block + (int64_t)r * stride + c4 * 4);
+    float* d = rowbuf + r * ldr + c4 * 4;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+}
+// rowbuf's 16 rows -> a contiguous [16][stride] block (all threads)
+__device__ __forceinline__ void store_rows16(const float* rowbuf, int ldr, int stride, float* __restrict__ block) {
+  const int v4 = stride >> 2;
+  for (int e = threadIdx.x; e < MDP_R * v4; e += blockDim.x) {
+    const int r = e / v4, c4 = e - r * v4;
+    const float* sp = rowbuf + r * ldr + c4 * 4;
+    *reinterpret_cast<float4*>(block + (int64_t)r * stride + c4 * 4) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+  }
+}
+
 __device__ __forceinline__ void copy_cols16(const float* src, int lds_src, int src_off, float* dst, int lds_dst, int dst_off,
                                    int ncols) {
   for (int e = threadIdx.x; e < MDP_R * ncols; e += blockDim.x) {

@@ -206,6 +206,7 @@ __device__ __forceinline__ void actor_pre_tile(const CriticArgs& a, float* lds, 
   float* dst = a.apre + (int64_t)r0 * MDP_APRE_W;
   for (int q = threadIdx.x; q < MDP_R * MDP_APRE_W / 4; q += blockDim.x)
     *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(apre_lds(q, h1a, h2a, lg, av));
+  store_rows16(rowbuf, ldr, T.row_stride, a.apre_rows + (int64_t)r0 * T.row_stride);
 }
 // float4 q of a row block [16][MDP_CPRE_W] <-> its LDS home (h1c | h2c | tacc | q + pad | a~ [16])
 __device__ __forceinline__ float* cpre_lds(int q, float* h1c, float* h2c, float* tacc, float* qv4, float* xa16) {
@@ -359,6 +360,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
   float* dst = a.cpre + (int64_t)r0 * MDP_CPRE_W;
   for (int q = threadIdx.x; q < MDP_R * MDP_CPRE_W / 4; q += blockDim.x)
     *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(cpre_lds(q, h1c, h2c, tacc, qv4, xa16));
+  store_rows16(rowbuf, ldr, T.row_stride, a.cpre_rows + (int64_t)r0 * T.row_stride);
 }
 }  // namespace
 
@@ -648,13 +650,15 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     __syncthreads();  // B4
     __syncthreads();  // B5: d2 ready
     dgrad_tile(d2, wt, h1c, d1, wave);
+    wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 0, 8);
     __syncthreads();  // B6
   } else {
     // ---------------- target critic Q'(o', a~), one 16-column tile per wave
     const int tt = wave - 4, col = 16 * tt + r;
     // the replay gather is issued first, by these waves only (their own weights are few
     // and needed late); waves 0..3 start on their weight loads at once
-    gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 256, 256);
+    if (post) load_rows16_part(a.cpre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 256, 256);
+    else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 256, 256);
     lds_signal(&rows_ready);
 #ifdef MDP_STAMPS
     if (tt == 0) {
@@ -695,12 +699,12 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     for (int i = 0; i < 4; ++i) h2t[(kq * 4 + i) * LH + col] = fmaxf(acc[i] + b2, 0.f);
     __syncthreads();  // B4
     if (tt == 0) MDP_STAMPW(6);
+    double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;  // wave 4's loss / stat partials (rows = lanes)
     if (tt == 0) {
       // fp64 TD target (maddpg.py:186), loss partials, dL/dq = 2 (q - y) / B
       const float qt = rq_head(h2t, LH, w3) + b3;
       if ((lane & 3) == 0) qn[lane >> 2] = qt;
       wave_sync();
-      double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;
       float g = 0.f;
       if (lane < nvalid) {
         const double rew = (double)rowbuf[lane * ldr + ag.rew_off];
@@ -717,6 +721,26 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         y_out[r0 + lane] = y64;
       }
       if (lane < MDP_R) dq[lane] = g;
+      MDP_STAMPW(60);
+      wave_sync();
+      // dW3 = h2^T dq, db3 = sum dq, d2 = (dq W3^T) o [h2 > 0]   (lane = hidden unit)
+      float s = 0.f, sb = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < MDP_R; ++rr) {
+        const float h = h2c[rr * LH + lane], dqr = dq[rr];
+        s = fmaf(h, dqr, s);
+        sb += dqr;
+        d2[rr * LD + lane] = h > 0.f ? dqr * w3c : 0.f;
+      }
+      MDP_STAMPW(61);
+      slab_st(slab + nd.t[4].off + lane, s);
+      if (lane == 0) slab_st(slab + nd.t[5].off, sb);
+      MDP_STAMPW(7);
+    }
+    __syncthreads();  // B5
+    if (tt == 0) {
+      MDP_STAMPW(8);
+      // the update's stats (maddpg.py:196): partial sums of this tile, beside the backward
       s_l = sum16(s_l);
       s_y = sum16(s_y);
       s_r = sum16(s_r);
@@ -728,24 +752,9 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         st[2] = s_r;
         st[3] = s_q;
       }
-      wave_sync();
-      // dW3 = h2^T dq, db3 = sum dq, d2 = (dq W3^T) o [h2 > 0]   (lane = hidden unit)
-      float s = 0.f, sb = 0.f;
-#pragma unroll
-      for (int rr = 0; rr < MDP_R; ++rr) {
-        const float h = h2c[rr * LH + lane], dqr = dq[rr];
-        s = fmaf(h, dqr, s);
-        sb += dqr;
-        d2[rr * LD + lane] = h > 0.f ? dqr * w3c : 0.f;
-      }
-      slab_st(slab + nd.t[4].off + lane, s);
-      if (lane == 0) slab_st(slab + nd.t[5].off, sb);
-      MDP_STAMPW(7);
     }
-    __syncthreads();  // B5
-    if (tt == 0) MDP_STAMPW(8);
-    // dW2 = h1^T d2 (waves 4..7), db2 = column sums of d2
-    wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 4, 4);
+    // dW2 = h1^T d2 over all waves (tiles w, w + 8; waves 0..3 after their dh1 tile), db2
+    wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 0, 8);
     if (tt == 1) colsum64(d2, LD, slab + nd.t[3].off);
     __syncthreads();  // B6
     if (tt == 0) MDP_STAMPW(9);
@@ -891,7 +900,10 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     } else {
       // ---------------- critic (post-step weights) forward with a_i = the sample (maddpg.py:48-52)
       // waves 2, 3 gather their share of the replay rows first
-      if (wave > 1) gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
+      if (wave > 1) {
+        if (a.apre) load_rows16_part(a.apre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 128, 384);
+        else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
+      }
       if (wave > 1) lds_signal(&rows_ready);
       const int k0 = KC * (wave - 1);  // this wave's third of the replay-part contraction
       f32x4 w1[KSC];
@@ -906,9 +918,12 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       rt_load<16>(w2t, P + nc.t[2].off, RH, 16 * wave + r, RH);
       const float b2t = P[nc.t[3].off + 16 * wave + r], w3t = P[nc.t[4].off + 16 * wave + r];
       lds_wait(&rows_ready, 6);
+      if (wave == 1) MDP_STAMPW(56);
       f32x4 acc[4];
       rf_zero(acc);
       if (k0 < ka_c) rf_acc<KSC>(acc, rowbuf + xo_c + k0, ldr, min(ka_c - k0, KC), w1);
+      if (wave == 1) MDP_STAMPW(57);
+      if (wave == 3) MDP_STAMPW(58);
       if (wave > 1) {  // hand the partial accumulators to wave 1 (lane-major, 16 floats each)
         float* pp = l1part + ((wave - 2) * 64 + lane) * 16;
 #pragma unroll
@@ -945,7 +960,8 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     // ---------------- dgrad tiles: dh1c through the critic, dh1a through the actor
     const int tt = wave - 4;
     // waves 2..7 gather the replay rows (first); waves 0, 1 start on their weights at once
-    gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
+    if (a.apre) load_rows16_part(a.apre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 128, 384);
+    else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
     lds_signal(&rows_ready);
     f32x4 wc[4], wa[4];
     rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);

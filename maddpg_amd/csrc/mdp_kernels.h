@@ -37,6 +37,7 @@ struct CriticArgs {
   // weights, which the critic step does not touch) into apre [B][MDP_APRE_W];
   // u_act: injected uniforms of that sample or null (0: no extra workgroups)
   float* apre;
+  float* apre_rows;     // the replay rows it gathered, [B][row_stride] (the actor step reads them contiguously)
   const float* u_act;
   // critic_post mode (k_critic_grad_r): the work of this critic step that does
   // not depend on the previous agent's update (target actors j != cpre_prev,
@@ -45,6 +46,7 @@ struct CriticArgs {
   // launch into cpre [B][MDP_CPRE_W]; only target actor cpre_prev (Polyak-
   // updated since) and the rest of the step remain (null: the full step)
   const float* cpre;
+  const float* cpre_rows;  // the replay rows the critic_pre gathered, [B][row_stride]
   int cpre_prev;
 };
 
@@ -78,9 +80,11 @@ struct ActorArgs {
   int multi;                  // throughput mode, as CriticArgs
   int64_t slab_agent_stride;
   const float* apre;          // k_actor_grad_r: the forward precomputed by the critic launch, or null
+  const float* apre_rows;     // ... and its replay rows [B][row_stride] (read instead of a gather)
   // k_actor_grad_r: B/16 extra workgroups run the NEXT critic step's
   // independent work (agent cpre_agent, indices cpre_idx) into cpre (null: none)
   float* cpre;
+  float* cpre_rows;
   int cpre_agent;
   const int32_t* cpre_idx;
   const float* target;        // target nets (the critic_pre role's target actors / critic)

@@ -77,6 +77,12 @@ if fast and st[48]:
     print("critic_post from start: w0 loads issued %.2f, rows %.2f, L1 tile %.2f, L2 tiles all %.2f, head+gumbel %.2f, "
           "B2 %.2f | w3 cpre loaded %.2f, w3 L2 tile %.2f us" % tuple(
               (st[i] - st[0]) * 10 / 1000 for i in (48, 49, 50, 51, 52, 53, 54, 55)))
+if fast and st[60]:
+    print("critic TD phase (w4): B4 -> dq %.2f, d2/dW3 loop %.2f, stats sums + stores %.2f us" % (
+        (st[60] - st[6]) * 10 / 1000, (st[61] - st[60]) * 10 / 1000, (st[7] - st[61]) * 10 / 1000))
+if fast and st[56]:
+    print("actor step from start: w1 rows ready %.2f, w1 L1 third done %.2f, w3 L1 third done %.2f us" % tuple(
+        (st[i] - st[16]) * 10 / 1000 for i in (56, 57, 58)))
 lib_ra = getattr(lib, "mdp_debug_stamps_ra", None)
 if lib_ra is not None:
     lib_ra.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
