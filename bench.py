@@ -63,11 +63,24 @@ def bytes_rollout(eng):
 
 def roofline_for(kind, eng, ms_avg):
     tp = getattr(eng, "update_mode", "strict") == "throughput"   # one launch serves every agent
+    suffix = "_r" if eng.lib.mdp_grad_variant(eng.h, 0) == 1 else ""
+    if kind == "grads":
+        # the critic-step and actor-step launches of one agent's update, together:
+        # each launch also runs part of the OTHER step (the actor step's forward
+        # rides in the critic launch, the next critic step's independent part in
+        # the actor launch), so the algorithmic flops are attributed to the pair
+        fl = sum(flops_critic_grad(eng, i) + flops_actor_grad(eng, i) for i in range(eng.n)) / (1 if tp else eng.n)
+        ach = fl / (ms_avg * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 4), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 6), "traffic": None,
+                "kernel": f"k_critic_grad{suffix}+k_actor_grad{suffix}", "kernels": [f"k_critic_grad{suffix}",
+                                                                               f"k_actor_grad{suffix}"],
+                "algorithmic_per_launch": fl, "avg_launch_ms": ms_avg,
+                "launch_unit": "one critic-step launch + one actor-step launch (one agent's update)"}
     if kind in ("critic_grad", "actor_grad"):
         f = flops_critic_grad if kind == "critic_grad" else flops_actor_grad
         fl = sum(f(eng, i) for i in range(eng.n)) / (1 if tp else eng.n)
         ach = fl / (ms_avg * 1e-3) / 1e12
-        suffix = "_r" if eng.lib.mdp_grad_variant(eng.h, 0) == 1 else ""
         return {"bound": "mfma", "achieved": round(ach, 4), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 6), "traffic": None,
                 "kernel": f"k_{kind}{suffix}", "algorithmic_per_launch": fl, "avg_launch_ms": ms_avg}
@@ -331,10 +344,16 @@ def main():
     per_kind = {k: eng.prof_read(k) for k in kinds}
     for k in kinds:
         eng.prof_enable(k, False)
-    # the dominant kernel among those with a roofline model (grads: MFMA, rollout: HBM)
-    modelled = [k for k in ("critic_grad", "actor_grad", "rollout", "reduce_apply") if per_kind[k][1]]
+    # the dominant kernel among those with a roofline model (the gradient launch
+    # pair: MFMA; rollout, optimizer step: HBM)
+    if per_kind["critic_grad"][1] and per_kind["critic_grad"][1] == per_kind["actor_grad"][1]:
+        per_kind["grads"] = (per_kind["critic_grad"][0] + per_kind["actor_grad"][0], per_kind["critic_grad"][1])
+    modelled = [k for k in ("grads", "rollout", "reduce_apply") if per_kind.get(k, (0, 0))[1]]
     ev_pre = event_overhead_ms(eng.stream)
-    dominant = max(modelled, key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_pre) if modelled else None
+    # (a pair carries two event pairs' overhead per "launch")
+    evn = {"grads": 2}
+    dominant = max(modelled, key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_pre * evn.get(k, 1)) \
+        if modelled else None
     ms_tot, launches = per_kind[dominant] if dominant else (0.0, 0)
 
     # secondary figure: the same workload in throughput mode (every
@@ -381,17 +400,29 @@ def main():
     roof = None
     if launches:
         raw = ms_tot / launches
-        roof = roofline_for(dominant, eng, max(raw - ev_ms, 1e-6))
+        roof = roofline_for(dominant, eng, max(raw - ev_ms * evn.get(dominant, 1), 1e-6))
         roof["dominant_of_all_kinds"] = max(
-            (k for k in per_kind if per_kind[k][1]), key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_ms)
+            (k for k in per_kind if per_kind[k][1] and k != "grads"),
+            key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_ms)
         roof["avg_launch_ms_raw_events"] = raw
         roof["event_pair_overhead_ms"] = ev_ms
         roof["launches_timed"] = launches
     cfg_key = f"{args.scenario}_E{args.num_envs}_B{args.batch_size}_H{args.num_units}"
     if args.num_agents is not None:
         cfg_key += f"_N{args.num_agents}"
-    if roof is not None:
+    if roof is not None and "kernels" in roof:
+        # the pair: HBM bytes and MFMA busy cycles of both kernels, durations summed
+        parts = [load_pmc(k, cfg_key) for k in roof["kernels"]]
+        pmc = {}
+        if all(p.get("hbm_bytes_per_launch") is not None for p in parts):
+            pmc["hbm_bytes_per_launch"] = sum(p["hbm_bytes_per_launch"] for p in parts)
+        if all(p.get("avg_ns") for p in parts):
+            pmc["avg_ns"] = sum(p["avg_ns"] for p in parts)
+            if all(p.get("mfma_busy_frac") is not None for p in parts):
+                pmc["mfma_busy_frac"] = sum(p["mfma_busy_frac"] * p["avg_ns"] for p in parts) / pmc["avg_ns"]
+    elif roof is not None:
         pmc = load_pmc(roof["kernel"], cfg_key)
+    if roof is not None:
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
         if pmc.get("mfma_busy_frac") is not None:
             # SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), profiles/<tag>_mfma.csv
@@ -436,8 +467,8 @@ def main():
             "dp_check": dp_check,
             "kernel_pass": {"steps": prof_steps, "event_pair_overhead_ms": round(ev_ms, 5),
                             "per_kind_ms_per_launch": {k: round(v[0] / v[1] - ev_ms, 5) for k, v in per_kind.items()
-                                                       if v[1]},
-                            "per_kind_launches": {k: v[1] for k, v in per_kind.items()}},
+                                                       if v[1] and k != "grads"},
+                            "per_kind_launches": {k: v[1] for k, v in per_kind.items() if k != "grads"}},
             "roofline": roof,
             "throughput_mode": tp_fig,
         }

@@ -209,6 +209,14 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     red[grp][col] = s;
     __syncthreads();
     MDP_STAMP(31);
+    if (grp == 0 && f.phase != 1 && a.stats_mode) {
+      // arrival: this workgroup has its step's beta powers and epochs in
+      // registers (loaded first, vmcnt drained), so the stats workgroup may
+      // advance them -- a fire-and-forget add instead of a returning atomic at
+      // the end of every workgroup
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(f.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (grp == 0) {
       f32x4 g = red[0][col];
 #pragma unroll
@@ -356,8 +364,36 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
   }
   MDP_STAMP(33);
   if (f.phase == 1) return;  // uniform: the whole grid of a reduce-only pass
-  // the last workgroup to finish advances the optimizer step (every net
-  // workgroup read beta before its add, so nobody reads the new values here)
+  if (a.stats_mode) {
+    // the stats workgroup advances the optimizer step once every chunk
+    // workgroup has arrived (read this step's beta powers and epochs); the
+    // grid is co-resident (mdp_ra_fits), the wait bounded
+    if (b == f.rblk[6] + (a.polyak ? a.oblk[6] : 0) && tid == 0) {
+      const uint32_t want = (uint32_t)f.rblk[6];
+      uint32_t it = 0;
+      while (__hip_atomic_load(f.done_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > kSpinLimit) {
+          __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __hip_atomic_store(f.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        const float p1 = a.beta[0], p2 = a.beta[1];
+        a.beta[2] = p1;
+        a.beta[3] = p2;
+        a.beta[0] = p1 * a.b1;
+        a.beta[1] = p2 * a.b2;
+      }
+      if (a.bump_ctr) a.ctl->upd_ctr += (uint32_t)a.bump_ctr;
+      if (f.phase == 3) f.xstep[0] += 1u;
+      f.sync_ctr[7 * 32] += 1u;
+    }
+    return;
+  }
+  // (no stats workgroup) the last workgroup to finish advances the optimizer
+  // step (every net workgroup read beta before its add)
   __syncthreads();
   if (tid == 0) {
     const uint32_t prev = __hip_atomic_fetch_add(f.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
