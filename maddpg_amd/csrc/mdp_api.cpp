@@ -625,6 +625,9 @@ FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net) {
   f.xd = nullptr;
   f.net_id = g;
   f.xstep = nullptr;
+  f.pf_count = 0;
+  f.pf_out = nullptr;
+  f.pf_ctl = h->ctl;
   return f;
 }
 
@@ -652,8 +655,13 @@ void xgmi_release(mdp_handle* h) {
   h->x_rank = 0;
 }
 
-int do_reduce_apply(mdp_handle* h, int agent, int net) {
+// pf_out / pf_count: a piece of the next round's index draw rides in this launch
+int do_reduce_apply(mdp_handle* h, int agent, int net, int32_t* pf_out = nullptr, int pf_count = 0) {
   FusedApplyArgs f = fused_args_for(h, agent, net);
+  if (pf_out && pf_count > 0) {
+    f.pf_out = pf_out;
+    f.pf_count = pf_count;
+  }
   if (h->p2p) set_xchg(h, f, agent, net);
   ProfScope p(h, MDP_K_REDUCE_APPLY);
   HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
@@ -747,16 +755,22 @@ bool critic_pre_ok(const mdp_handle* h, int p, int k) {
 
 // strict data-parallel update of one agent (maddpg.py:188-194 order):
 // critic grads -> reduce -> all-reduce -> clip + Adam (x 1/G); then the actor
+// the next round's draw in pieces inside the optimizer launches (general kernels)
+struct DrawPieces {
+  int32_t* out = nullptr;   // this agent's critic-step piece; the actor-step piece follows it
+  int n_critic = 0, n_actor = 0;
+};
+
 int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out, int post_prev, int pre_next,
-                 const int32_t* pre_idx) {
+                 const int32_t* pre_idx, const DrawPieces& dp) {
   const float scale = 1.0f / (float)h->dp_world;
   const bool pre = actor_pre_ok(h, agent);
   int rc;
   if (h->p2p) {  // the exchange lives inside the optimizer launch: same 4 launches as one GPU
     if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre, nullptr, post_prev))) return rc;
-    if ((rc = do_reduce_apply(h, agent, 1))) return rc;
+    if ((rc = do_reduce_apply(h, agent, 1, dp.out, dp.n_critic))) return rc;
     if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre, pre_next, pre_idx))) return rc;
-    return do_reduce_apply(h, agent, 0);
+    return do_reduce_apply(h, agent, 0, dp.out ? dp.out + dp.n_critic : nullptr, dp.n_actor);
   }
   if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre, nullptr, post_prev))) return rc;
   if ((rc = do_reduce(h, agent, 1))) return rc;
@@ -773,22 +787,23 @@ int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out, 
 // actor launch started (critic_post); pre_next >= 0: this actor launch starts
 // agent pre_next's next critic step on indices pre_idx (critic_pre)
 int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act,
-              int32_t* pf_out = nullptr, int post_prev = -1, int pre_next = -1, const int32_t* pre_idx = nullptr) {
+              int32_t* pf_out = nullptr, int post_prev = -1, int pre_next = -1, const int32_t* pre_idx = nullptr,
+              const DrawPieces& dp = DrawPieces()) {
   if ((h->comm || h->p2p) && !u_tgt && !u_act)
-    return do_update_dp(h, agent, idx, pf_out, post_prev, pre_next, pre_idx);
+    return do_update_dp(h, agent, idx, pf_out, post_prev, pre_next, pre_idx, dp);
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
   const bool pre = actor_pre_ok(h, agent);
   if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev))) return rc;
   if (fused) {
-    if ((rc = do_reduce_apply(h, agent, 1))) return rc;
+    if ((rc = do_reduce_apply(h, agent, 1, dp.out, dp.n_critic))) return rc;
   } else {
     if ((rc = do_reduce(h, agent, 1))) return rc;
     if ((rc = do_apply(h, agent, 1, false, 1.0f))) return rc;
   }
   if ((rc = do_actor_grad(h, agent, idx, u_act, false, pre, pre_next, pre_idx))) return rc;
   if (fused) {
-    if ((rc = do_reduce_apply(h, agent, 0))) return rc;
+    if ((rc = do_reduce_apply(h, agent, 0, dp.out ? dp.out + dp.n_critic : nullptr, dp.n_actor))) return rc;
   } else {
     if ((rc = do_reduce(h, agent, 0))) return rc;
     if ((rc = do_apply(h, agent, 0, false, 1.0f))) return rc;
@@ -1411,13 +1426,24 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
 // round's indices, if drawn by now (the prefetch in agent 0's critic launch),
 // lets this round's last actor launch do the next round's agent-0 part.
 // Returns in *carry_out whether it did.
+// draw_out: the next round's n*B indices drawn in 2n pieces by the round's
+// optimizer launches (configurations without the fast critic kernel's
+// prefetch; only where every step is the one-launch fused kind)
 static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nullptr, bool carry_in = false,
-                         const int32_t* next_idx = nullptr, bool* carry_out = nullptr) {
+                         const int32_t* next_idx = nullptr, bool* carry_out = nullptr, int32_t* draw_out = nullptr) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   if (carry_out) *carry_out = false;
   if (h->update_mode == 1) return do_round_tp(h, idx, nullptr, nullptr, pf_out);
+  const int nb = n * B, piece = (nb + 2 * n - 1) / (2 * n);
   int rc = 0;
   for (int i = 0; i < n && !rc; ++i) {
+    DrawPieces dp;
+    if (draw_out) {
+      const int o = std::min(nb, 2 * i * piece);
+      dp.out = draw_out + o;
+      dp.n_critic = std::min(piece, nb - o);
+      dp.n_actor = std::min(piece, nb - o - dp.n_critic);
+    }
     const int post_prev = i > 0 ? (critic_pre_ok(h, i - 1, i) ? i - 1 : -1) : (carry_in ? n - 1 : -1);
     int pre_next = -1;
     const int32_t* pre_idx = nullptr;
@@ -1430,9 +1456,17 @@ static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nu
       if (carry_out) *carry_out = true;
     }
     rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, i == 0 ? pf_out : nullptr, post_prev, pre_next,
-                   pre_idx);
+                   pre_idx, dp);
   }
   return rc;
+}
+
+// can the round's optimizer launches draw the next round's indices (all fused)?
+static bool draw_in_ra_ok(const mdp_handle* h) {
+  if (!h->fused_apply || h->comm) return false;
+  for (int i = 0; i < h->cfg.n_agents; ++i)
+    if (!reduce_apply_ok(h, i, 0) || !reduce_apply_ok(h, i, 1)) return false;
+  return true;
 }
 
 // can agent 0's critic kernel draw the next round's indices on the side?
@@ -1816,11 +1850,12 @@ static int step_launches(mdp_handle* h, int rounds) {
   const bool pf = prefetch_ok(h);
   if (!in_rollout && (rc = launch_make_index(h, nb, slot[0]))) return rc;
   bool carry = false;
+  const bool ra_draw = !pf && h->update_mode == 0 && draw_in_ra_ok(h);
   for (int r = 0; r < rounds && !rc; ++r) {
     const bool more = r + 1 < rounds;
     int32_t* next = (more && pf) ? slot[(r + 1) & 1] : nullptr;  // drawn in agent 0's critic launch
-    rc = round_updates(h, slot[r & 1], next, carry, next, &carry);
-    if (!rc && more && !pf) rc = launch_make_index(h, nb, slot[(r + 1) & 1]);
+    rc = round_updates(h, slot[r & 1], next, carry, next, &carry, (more && ra_draw) ? slot[(r + 1) & 1] : nullptr);
+    if (!rc && more && !pf && !ra_draw) rc = launch_make_index(h, nb, slot[(r + 1) & 1]);
   }
   return rc;
 }

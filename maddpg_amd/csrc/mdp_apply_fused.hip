@@ -27,6 +27,7 @@
 // AdamOptimizer._finish update) and, for the actor step, the noise counter.
 #include "mdp_device.h"
 #include "mdp_kernels.h"
+#include "mdp_mt.h"
 
 namespace {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -413,7 +414,11 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
 }
 
 __global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
-  reduce_apply_body(f, blockIdx.x, gridDim.x);
+  if (f.pf_count > 0 && blockIdx.x == gridDim.x - 1) {  // a piece of the next round's index draw
+    make_index_block<1024>(f.pf_ctl, f.pf_count, f.pf_out);
+    return;
+  }
+  reduce_apply_body(f, blockIdx.x, gridDim.x - (f.pf_count > 0 ? 1 : 0));
 }
 
 // throughput mode: the steps of several nets in one launch (each net's chunk
@@ -431,7 +436,7 @@ int mdp_ra_grid(const FusedApplyArgs& f) {
 }
 
 hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_apply, dim3(mdp_ra_grid(f)), dim3(1024), 0, s, f);
+  hipLaunchKernelGGL(k_reduce_apply, dim3(mdp_ra_grid(f) + (f.pf_count > 0 ? 1 : 0)), dim3(1024), 0, s, f);
   return hipGetLastError();
 }
 

@@ -166,6 +166,12 @@ struct FusedApplyArgs {
   const XchgDesc* xd;   // phase 3: device copy of the exchange descriptor
   int net_id;           // phase 3: 2 * agent + net (epoch counter)
   uint32_t* xstep;      // phase 3: Ctl::xstep[net_id], exchanges done for this net
+  // > 0: one extra (last) workgroup draws pf_count indices of the NEXT round
+  // into pf_out, continuing the MT19937 stream (a piece of the draw the fast
+  // kernels make beside the critic step; general-kernel configurations)
+  int pf_count;
+  int32_t* pf_out;
+  Ctl* pf_ctl;
 };
 // sync area: per (agent, net) 8 counters x 128 B (6 done, 7 norm epoch), then [6][MAXCH][2] tagged words
 inline int64_t mdp_ra_sync_bytes() {
@@ -316,7 +322,7 @@ hipError_t mdp_ra_occupancy(int* per_cu);   // co-resident k_reduce_apply workgr
 inline int mdp_ra_grid_of(const Topo& t, int agent, int net) {
   const NDesc& d = net ? t.ag[agent].critic : t.ag[agent].actor;
   const NDesc& o = net ? t.ag[agent].actor : t.ag[agent].critic;
-  int g = 1;
+  int g = 2;  // + the stats workgroup and a slot for an index-draw workgroup
   for (int k = 0; k < 6; ++k) {
     g += (d.t[k].rows * d.t[k].cols + MDP_RA_CHUNK - 1) / MDP_RA_CHUNK;
     if (!net) g += (o.t[k].rows * o.t[k].cols + MDP_APPLY_CHUNK - 1) / MDP_APPLY_CHUNK;

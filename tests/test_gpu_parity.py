@@ -563,14 +563,17 @@ def test_rollout_policy_actions_match_oracle():
         np.testing.assert_allclose(rows[:, lay[j]["act"]:lay[j]["act"] + ACT], want, atol=2e-6)
 
 
-@pytest.mark.parametrize("cap", [20000, 3300])
-def test_train_step_graph_equals_step_then_rounds(cap):
+@pytest.mark.parametrize("cap,general", [(20000, False), (3300, False), (20000, True)])
+def test_train_step_graph_equals_step_then_rounds(monkeypatch, cap, general):
     """mdp_train_step(k) (rollout + k rounds replayed as one graph; the first
-    round's indices drawn by an extra rollout workgroup) is the same work as
-    env_step + k x update_round: bit-identical state and RNG stream after 4
-    steps.  cap=3300: the ring fills during the steps (draws against the
-    capped length)."""
+    round's indices drawn by an extra rollout workgroup, the later rounds' by
+    the fast critic kernel -- or, on the general kernels, in pieces by the
+    optimizer launches) is the same work as env_step + k x update_round:
+    bit-identical state and RNG stream after 4 steps.  cap=3300: the ring
+    fills during the steps (draws against the capped length)."""
     from maddpg_amd.runner import VecRunner
+    if general:
+        monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
 
     def make():
         r = VecRunner("simple_spread", 64, batch_size=128, capacity=cap, seed=3, train_every=16)

@@ -232,14 +232,15 @@ def test_optimizer_coresidency_plan():
     lib = _lib.load()
     out = (ctypes.c_int32 * 16)()
     # S2 at H=64, chunks of 256 per tensor: critic W1 18 + b1 1 + W2 16 + b2 1 +
-    # W3 1 + b3 1 + stats 1 = 39; actor 5 + 1 + 16 + 1 + 2 + 1 = 26, + 13 Polyak
-    # workgroups of the critic (1,024-parameter chunks) + stats = 40 (3 agents)
+    # W3 1 + b3 1 + stats 1 + a slot for an index-draw workgroup = 40; actor 5 +
+    # 1 + 16 + 1 + 2 + 1 = 26, + 13 Polyak workgroups of the critic (1,024-
+    # parameter chunks) + stats + draw slot = 41 (3 agents)
     assert lib.mdp_ra_plan(ctypes.byref(_cfg()), 256, 1, out) == 0
-    assert list(out[:6]) == [40, 39] * 3
-    # the same launch on a device holding 39 workgroups: the actor steps fall back
-    assert lib.mdp_ra_plan(ctypes.byref(_cfg()), 39, 1, out) == 3
-    assert list(out[:6]) == [-40, 39] * 3
-    # H=256: the 256x256 W2 alone is 256 chunks -> every critic step (330
+    assert list(out[:6]) == [41, 40] * 3
+    # the same launch on a device holding 40 workgroups: the actor steps fall back
+    assert lib.mdp_ra_plan(ctypes.byref(_cfg()), 40, 1, out) == 3
+    assert list(out[:6]) == [-41, 40] * 3
+    # H=256: the 256x256 W2 alone is 256 chunks -> every critic step (331
     # workgroups) and actor step exceed 256 slots
     n = lib.mdp_ra_plan(ctypes.byref(_cfg(num_units=256)), 256, 1, out)
     assert n == 6 and all(v < 0 for v in out[:6]) and -out[1] > 256
