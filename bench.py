@@ -298,6 +298,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    dt_local = dt
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -308,7 +309,7 @@ def main():
         # exchange ran over, and bit-identical replicas (strict data parallelism
         # keeps every rank's weights, targets, Adam moments and beta powers equal)
         r.synchronize()
-        info = {"ms_per_step": round(dt / args.steps * 1e3, 4), "checksum": eng.param_checksum(),
+        info = {"ms_per_step": round(dt_local / args.steps * 1e3, 4), "checksum": eng.param_checksum(),
                 "dp": eng.dp_info() if getattr(r, "native_dp", False) else {"kind": r.dp_kind, "ranks": world}}
         allinfo = [None] * world
         dist.all_gather_object(allinfo, info)

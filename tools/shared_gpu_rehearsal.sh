@@ -19,9 +19,9 @@ run() {  # name nproc env-assignment [bench args...]
   echo "$name: $(tail -c 400 $O/$name.json)"
 }
 run xgmi2 2 MDP_DP_XGMI=1
-run xgmi4 4 MDP_DP_XGMI=1
+run xgmi4 4 MDP_DP_XGMI=1 --no-throughput-figure
 run torchdist2 2 MDP_NATIVE_DP=0
 # configs[4]'s topology (general H=128 kernels), 2 ranks over xGMI
 run tag6_xgmi2 2 MDP_DP_XGMI=1 --scenario simple_tag --num-agents 6 --scenario-adversaries 4 \
-    --num-adversaries 4 --num-units 128 --batch-size 4096 --num-envs 4096 --steps 5
+    --num-adversaries 4 --num-units 128 --batch-size 4096 --num-envs 4096 --steps 5 --no-throughput-figure
 echo "rehearsal $TAG done"
