@@ -295,28 +295,31 @@ def main():
     for _ in range(args.steps):
         rounds += one_step()
     torch.cuda.synchronize()
+    dt_local = time.perf_counter() - t0     # this rank's own finish, before the closing barrier
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt_local = dt
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    dp_check = None
+    # the run validates itself: every rank's ms/step, the communicator the
+    # exchange ran over, and bit-identical replicas (strict data parallelism
+    # keeps every rank's weights, targets, Adam moments and beta powers equal).
+    # At N=1 the same fields describe the single replica (no communicator).
+    r.synchronize()
+    info = {"ms_per_step": round(dt_local / args.steps * 1e3, 4), "checksum": eng.param_checksum()}
     if world > 1:
-        # the run validates itself: every rank's ms/step, the communicator the
-        # exchange ran over, and bit-identical replicas (strict data parallelism
-        # keeps every rank's weights, targets, Adam moments and beta powers equal)
-        r.synchronize()
-        info = {"ms_per_step": round(dt_local / args.steps * 1e3, 4), "checksum": eng.param_checksum(),
-                "dp": eng.dp_info() if getattr(r, "native_dp", False) else {"kind": r.dp_kind, "ranks": world}}
+        info["dp"] = eng.dp_info() if getattr(r, "native_dp", False) else {"kind": r.dp_kind, "ranks": world}
         allinfo = [None] * world
         dist.all_gather_object(allinfo, info)
-        dp_check = {"replicas_identical": all(x["checksum"] == allinfo[0]["checksum"] for x in allinfo),
-                    "per_rank_ms_per_step": [x["ms_per_step"] for x in allinfo],
-                    "communicator": allinfo[0]["dp"],
-                    "peers_per_rank": [x["dp"].get("peers") for x in allinfo]}
+    else:
+        info["dp"] = {"kind": "none", "ranks": 1, "rank": 0, "peers": 0}
+        allinfo = [info]
+    dp_check = {"replicas_identical": all(x["checksum"] == allinfo[0]["checksum"] for x in allinfo),
+                "per_rank_ms_per_step": [x["ms_per_step"] for x in allinfo],
+                "communicator": allinfo[0]["dp"],
+                "peers_per_rank": [x["dp"].get("peers") for x in allinfo]}
     # second figure: rollout only (actors + Gumbel + MPE physics + replay
     # append) over the same env copies, no training
     ro_steps = max(10, args.steps)
