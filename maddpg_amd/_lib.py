@@ -158,6 +158,8 @@ def load():
             "(or __graft_entry__.build()); maddpg_amd has no CPU fallback")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("MDP_LIB") and not hasattr(lib, name):
+            continue  # an explicitly chosen other build (A/B of an older one): entry points it lacks stay unbound
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
