@@ -114,6 +114,10 @@ __host__ __device__ __forceinline__ int lds_ld(int cols) { return (cols | 1); }
 // N multiple of 16.  Column tiles are dealt round-robin over the 4 waves.
 // B fragments of one 64-deep K chunk (16 MFMA k-steps) for one column: all 16
 // global loads are issued together so the chunk pays one L2 latency, not 16.
+// Rows k >= K load the (finite) row K-1 and are NOT zeroed here: the consumer
+// zeroes the A operand of those rows (mfma_chunk / load_afrag).  A select on
+// the loaded value would make the wave wait for the load right where it is
+// issued -- the prefetch of the next chunk would not overlap the current one.
 #define MDP_KC 16
 __device__ __forceinline__ void load_wchunk(float (&w)[MDP_KC], const float* __restrict__ W, int ldw, int col, int c0,
                                    int K, int kq) {
@@ -121,8 +125,7 @@ __device__ __forceinline__ void load_wchunk(float (&w)[MDP_KC], const float* __r
 #pragma unroll
   for (int s = 0; s < MDP_KC; ++s) {
     const int k = c0 + 4 * s + kq;
-    const float v = W[min(k, kmax) * ldw + col];
-    w[s] = k < K ? v : 0.f;
+    w[s] = W[min(k, kmax) * ldw + col];
   }
 }
 // same for a transposed operand: element (k, col) at W[col * ldw + k]
@@ -133,7 +136,7 @@ __device__ __forceinline__ void load_wchunk_t(float (&w)[MDP_KC], const float* _
   for (int s = 0; s < MDP_KC; ++s) {
     const int k = c0 + 4 * s + kq;
     const float v = W[col * ldw + min(k, kmax)];
-    w[s] = (k < K && colok) ? v : 0.f;
+    w[s] = colok ? v : 0.f;
   }
 }
 // acc += A[r][c0 .. c0+63] . w  with A from LDS (row r = lane&15)

@@ -82,14 +82,16 @@ struct TileJob {
 // flight of the 16-column version.  Units are dealt round-robin over the
 // waves; each walks its 4 KS-deep k-steps per chunk with the next chunk (of
 // this unit or of the wave's next unit) in flight.
+// rows k >= K: the clamped (finite) row K-1 is loaded and the A operand of
+// that row is zeroed in rg_acc -- no select on the loaded value, which would
+// make the wave wait for the prefetch right where it is issued
 template <int KS>
 __device__ __forceinline__ void rg_load(f32x4 (&w)[KS], const float* __restrict__ W, int N, int col4, int c0, int K,
                                         int kq) {
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k = c0 + 4 * s + kq;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(W + (int64_t)min(k, K - 1) * N + col4);
-    w[s] = k < K ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+    w[s] = *reinterpret_cast<const f32x4*>(W + (int64_t)min(k, K - 1) * N + col4);
   }
 }
 template <int KS>
@@ -97,7 +99,11 @@ __device__ __forceinline__ void rg_acc(f32x4 (&acc)[4], const float* X, int ldx,
                                        const f32x4 (&w)[KS]) {
   float x[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) x[s] = X[r * ldx + min(c0 + 4 * s + kq, K - 1)];
+  for (int s = 0; s < KS; ++s) {
+    const int k = c0 + 4 * s + kq;
+    const float v = X[r * ldx + min(k, K - 1)];
+    x[s] = k < K ? v : 0.f;
+  }
   __builtin_amdgcn_sched_barrier(0);  // every A read ahead of the MFMA chain
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
