@@ -742,31 +742,37 @@ struct LdsCarve {
 
 __device__ __forceinline__ f32x4 ld4(const float* __restrict__ p) { return *reinterpret_cast<const f32x4*>(p); }
 
-// w[s] = W[4s+kq][4r .. 4r+3] of W[K][64]; rows >= K or inside [mlo, mhi) read as zero
+// w[s] = W[4s+kq][4r .. 4r+3] of W[K][64] for the k-steps below K (others 0).
+// Rows >= K hold the clamped row K-1 and rows the caller excludes stay as
+// loaded: rf_acc zeroes the A operand of those rows.  (A select on the loaded
+// value inside the per-k-step branch made the wave wait for each load before
+// issuing the next: serialised round trips.)
 template <int KS>
-__device__ __forceinline__ void rf_load(f32x4 (&w)[KS], const float* __restrict__ W, int K, int mlo, int mhi) {
-  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+__device__ __forceinline__ void rf_load(f32x4 (&w)[KS], const float* __restrict__ W, int K) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  const int kq = lane >> 4;
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     w[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (4 * s < K) {
-      const int k = 4 * s + kq;
-      const f32x4 v = ld4(W + min(k, K - 1) * MDP_RH + 4 * r);
-      const bool z = k >= K || (k >= mlo && k < mhi);
-      w[s] = f32x4{z ? 0.f : v[0], z ? 0.f : v[1], z ? 0.f : v[2], z ? 0.f : v[3]};
-    }
+    if (4 * s < K) w[s] = ld4(W + min(4 * s + kq, K - 1) * MDP_RH + 4 * r);  // wave-uniform branch
   }
 }
 
-// acc[t] += X[16][K] @ W (the fragments of rf_load); X in LDS.  All A fragments
-// are read first (clamped, unconditional) so the MFMA chain never waits on LDS.
+// acc[t] += X[16][K] @ W (the fragments of rf_load); X in LDS; input rows >= K
+// and rows inside [mlo, mhi) contribute zero.  All A fragments are read first
+// (clamped, unconditional) so the MFMA chain never waits on LDS.
 template <int KS>
-__device__ __forceinline__ void rf_acc(f32x4 (&acc)[4], const float* X, int ldx, int K, const f32x4 (&w)[KS]) {
+__device__ __forceinline__ void rf_acc(f32x4 (&acc)[4], const float* X, int ldx, int K, const f32x4 (&w)[KS],
+                                       int mlo = 0, int mhi = 0) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const float* xr = X + r * ldx;
   float x[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) x[s] = xr[min(4 * s + kq, K - 1)];
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + kq;
+    const float v = xr[min(k, K - 1)];
+    x[s] = (k < K && (k < mlo || k >= mhi)) ? v : 0.f;
+  }
   __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMA chain
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -835,29 +841,23 @@ __device__ __forceinline__ float rq_head(const float* X, int ldx, const float (&
 }
 
 // one 16-column tile per wave (column col = 16 tt + r of W[K][ldw]), k = 4s + kq;
-// unconditional clamped loads (straight-line code, exact vmcnt accounting); K >= 1
+// unconditional clamped loads (straight-line code, exact vmcnt accounting); K >= 1.
+// Rows >= K hold the clamped row K-1: rt_acc zeroes their A operand.
 template <int KS>
 __device__ __forceinline__ void rt_load(float (&w)[KS], const float* __restrict__ W, int ldw, int col, int K) {
   const int kq = (threadIdx.x & 63) >> 4;
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = 4 * s + kq;
-    const float v = W[min(k, K - 1) * ldw + col];
-    w[s] = k < K ? v : 0.f;
-  }
+  for (int s = 0; s < KS; ++s) w[s] = W[min(4 * s + kq, K - 1) * ldw + col];
 }
-// rt_load for a runtime K <= 4 KS: only the k-steps below K issue loads
+// rt_load for a runtime K <= 4 KS: only the k-steps below K issue loads (no
+// select on the loaded value: it would serialise the loads, see rf_load)
 template <int KS>
 __device__ __forceinline__ void rt_load_k(float (&w)[KS], const float* __restrict__ W, int ldw, int col, int K) {
   const int kq = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     w[s] = 0.f;
-    if (4 * s < K) {  // wave-uniform
-      const int k = 4 * s + kq;
-      const float v = W[min(k, K - 1) * ldw + col];
-      w[s] = k < K ? v : 0.f;
-    }
+    if (4 * s < K) w[s] = W[min(4 * s + kq, K - 1) * ldw + col];  // wave-uniform branch
   }
 }
 template <int KS>
@@ -866,7 +866,11 @@ __device__ __forceinline__ void rt_acc(f32x4& acc, const float* X, int ldx, int 
   const float* xr = X + r * ldx;
   float x[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) x[s] = xr[min(4 * s + kq, K - 1)];
+  for (int s = 0; s < KS; ++s) {
+    const int k = 4 * s + kq;
+    const float v = xr[min(k, K - 1)];
+    x[s] = k < K ? v : 0.f;
+  }
   __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMA chain
 #pragma unroll
   for (int s = 0; s < KS; ++s)

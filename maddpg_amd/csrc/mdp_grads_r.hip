@@ -130,8 +130,8 @@ __device__ __forceinline__ void actor_fwd_wave(const float* __restrict__ P, cons
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   f32x4 w1[16], w2[16];
   float w3[16];
-  rf_load<16>(w1, P + na.t[0].off, ag.obs_dim, 0, 0);
-  rf_load<16>(w2, P + na.t[2].off, RH, 0, 0);
+  rf_load<16>(w1, P + na.t[0].off, ag.obs_dim);
+  rf_load<16>(w2, P + na.t[2].off, RH);
   rh_load(w3, P + na.t[4].off, MDP_ACT_DIM);
   const f32x4 b1 = ld4(P + na.t[1].off + 4 * r), b2 = ld4(P + na.t[3].off + 4 * r);
   const float b3 = P[na.t[5].off + min(r, MDP_ACT_DIM - 1)];
@@ -261,8 +261,8 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
       const NDesc& an = aj.actor;
       f32x4 w1[16], w2[16];
       float w3[16];
-      rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
-      rf_load<16>(w2, Pt + an.t[2].off, RH, 0, 0);
+      rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim);
+      rf_load<16>(w2, Pt + an.t[2].off, RH);
       rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
       const f32x4 b1 = ld4(Pt + an.t[1].off + 4 * r), b2 = ld4(Pt + an.t[3].off + 4 * r);
       const float b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
@@ -310,8 +310,8 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
   } else if (wave == 3) {
     f32x4 w1[20], w2[16];
     float w3[16];
-    rf_load<20>(w1, Pc + nd.t[0].off, ka_c, 0, 0);
-    rf_load<16>(w2, Pc + nd.t[2].off, RH, 0, 0);
+    rf_load<20>(w1, Pc + nd.t[0].off, ka_c);
+    rf_load<16>(w2, Pc + nd.t[2].off, RH);
     rq_load(w3, Pc + nd.t[4].off);
     const f32x4 b1 = ld4(Pc + nd.t[1].off + 4 * r), b2 = ld4(Pc + nd.t[3].off + 4 * r);
     const float b3 = Pc[nd.t[5].off];
@@ -542,8 +542,8 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 #endif
       f32x4 w1[16], w2[16];
       float w3[16];
-      rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim, 0, 0);
-      rf_load<16>(w2, Pt + an.t[2].off, RH, 0, 0);
+      rf_load<16>(w1, Pt + an.t[0].off, aj.obs_dim);
+      rf_load<16>(w2, Pt + an.t[2].off, RH);
       rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
       const f32x4 b1 = ld4(Pt + an.t[1].off + 4 * r), b2 = ld4(Pt + an.t[3].off + 4 * r);
       const float b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
@@ -615,9 +615,9 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       // ---------------- online critic forward q(o, a) (maddpg.py:85-88, 104)
       f32x4 w1[20], w1b[2], w2[16];
       float w3[16];
-      rf_load<20>(w1, Pc + nd.t[0].off, ka_c, 0, 0);
-      rf_load<2>(w1b, Pc + nd.t[0].off + ka_c * RH, kb_c, 0, 0);
-      rf_load<16>(w2, Pc + nd.t[2].off, RH, 0, 0);
+      rf_load<20>(w1, Pc + nd.t[0].off, ka_c);
+      rf_load<2>(w1b, Pc + nd.t[0].off + ka_c * RH, kb_c);
+      rf_load<16>(w2, Pc + nd.t[2].off, RH);
       rq_load(w3, Pc + nd.t[4].off);
       const f32x4 b1 = ld4(Pc + nd.t[1].off + 4 * r), b2 = ld4(Pc + nd.t[3].off + 4 * r);
       const float b3 = Pc[nd.t[5].off];
@@ -907,11 +907,10 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       if (wave > 1) lds_signal(&rows_ready);
       const int k0 = KC * (wave - 1);  // this wave's third of the replay-part contraction
       f32x4 w1[KSC];
-      rf_load<KSC>(w1, P + nc.t[0].off + k0 * RH, max(min(ka_c - k0, KC), 0), ag.a_in_off - k0,
-                   ag.a_in_off + MDP_ACT_DIM - k0);
+      rf_load<KSC>(w1, P + nc.t[0].off + k0 * RH, max(min(ka_c - k0, KC), 0));  // a_i rows: zeroed in rf_acc
       f32x4 w1b[2], b1;
       if (wave == 1) {
-        rf_load<2>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM, 0, 0);
+        rf_load<2>(w1b, P + nc.t[0].off + ag.a_in_off * RH, MDP_ACT_DIM);
         b1 = ld4(P + nc.t[1].off + 4 * r);
       }
       float w2t[16];  // critic L2 column tile `wave`
@@ -921,7 +920,9 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       if (wave == 1) MDP_STAMPW(56);
       f32x4 acc[4];
       rf_zero(acc);
-      if (k0 < ka_c) rf_acc<KSC>(acc, rowbuf + xo_c + k0, ldr, min(ka_c - k0, KC), w1);
+      if (k0 < ka_c)
+        rf_acc<KSC>(acc, rowbuf + xo_c + k0, ldr, min(ka_c - k0, KC), w1, ag.a_in_off - k0,
+                    ag.a_in_off + MDP_ACT_DIM - k0);
       if (wave == 1) MDP_STAMPW(57);
       if (wave == 3) MDP_STAMPW(58);
       if (wave > 1) {  // hand the partial accumulators to wave 1 (lane-major, 16 floats each)
