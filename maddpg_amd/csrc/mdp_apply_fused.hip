@@ -60,64 +60,69 @@ __device__ __forceinline__ uint64_t ll_word(float v, uint32_t ep) {
 // returns the sum over ranks in rank order (identical on every rank).  A
 // bounded wait (30 s on the 100 MHz real-time clock) records *fault = 2 and
 // gives up; once a fault is recorded later exchanges do not wait.
-__device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc& x, uint32_t* fault, f32x4 g, int64_t i0, bool act,
+// The descriptor is read into (uniform) registers once, before any atomic
+// (re-reading it after each one serialised a round trip per peer), and the
+// exchange words are addressed as global memory (not FLAT): every peer's
+// stores and every word's load issue back to back, one round trip per poll.
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc* xdp, uint32_t* fault, f32x4 g, int64_t i0, bool act,
                                            uint32_t ep) {
-  const int W = x.world, r = x.rank;
+  const int W = __builtin_amdgcn_readfirstlane(xdp->world), r = __builtin_amdgcn_readfirstlane(xdp->rank);
+  const int64_t pt = (int64_t)uni64((uint64_t)xdp->pt);
+  uint64_t base[MDP_XCH_MAXW];
+#pragma unroll
+  for (int q = 0; q < MDP_XCH_MAXW; ++q) base[q] = uni64((uint64_t)xdp->data[q]);  // all slots: no per-slot branch
   const int64_t slot_row = (int64_t)(ep & 1u) * W;
   if (act) {
-    uint64_t* mine = nullptr;
-    for (int q = 0; q < W; ++q) {
-      if (q == r) continue;
-      mine = x.data[q] + (slot_row + r) * x.pt + i0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        __hip_atomic_store(mine + j, ll_word(g[j], ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int q = 0; q < MDP_XCH_MAXW; ++q) {
+      if (q < W && q != r) {
+        gu64* dst = reinterpret_cast<gu64*>(base[q]) + (slot_row + r) * pt + i0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __hip_atomic_store(dst + j, ll_word(g[j], ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
   const bool gone = __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-  // every peer's 4 words in flight at once (one round trip for the whole world,
-  // not one per peer), then only the words still missing, again all at once
+  const gu64* mine = reinterpret_cast<const gu64*>(base[r]) + slot_row * pt + i0;
+  // every peer's 4 words in flight at once (one round trip for the whole
+  // world, not one per peer), re-read together until all carry this epoch
   float pv[MDP_XCH_MAXW][4];
-  uint32_t pend = 0;  // bit 4 q + j: word j of peer q not yet carrying this epoch
+  uint64_t t0 = 0;
+  while (true) {
+    uint64_t w[MDP_XCH_MAXW][4];
 #pragma unroll
-  for (int q = 0; q < MDP_XCH_MAXW; ++q) {
-    if (q < W && q != r && act) {
-      const uint64_t* src = x.data[r] + (slot_row + q) * x.pt + i0;
+    for (int q = 0; q < MDP_XCH_MAXW; ++q) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint64_t w = __hip_atomic_load(const_cast<uint64_t*>(src + j), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_SYSTEM);
-        pv[q][j] = __uint_as_float((uint32_t)w);
-        if ((uint32_t)(w >> 32) != ep) pend |= 1u << (4 * q + j);
+        w[q][j] = (uint64_t)ep << 32;
+        if (q < W && q != r && act)
+          w[q][j] = __hip_atomic_load(const_cast<gu64*>(mine + q * pt + j), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pv[q][j] = 0.f;
     }
-  }
-  uint64_t t0 = 0;
-  while (pend != 0u && !gone) {
+    bool all = true;
+#pragma unroll
+    for (int q = 0; q < MDP_XCH_MAXW; ++q) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pv[q][j] = __uint_as_float((uint32_t)w[q][j]);
+        all = all && (uint32_t)(w[q][j] >> 32) == ep;
+      }
+    }
+    if (all || gone) break;
     __builtin_amdgcn_s_sleep(1);
     if (t0 == 0) t0 = __builtin_amdgcn_s_memrealtime();
     if (__builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
       __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
-    uint32_t still = 0;
-#pragma unroll
-    for (int q = 0; q < MDP_XCH_MAXW; ++q) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (pend & (1u << (4 * q + j))) {
-          const uint64_t* src = x.data[r] + (slot_row + q) * x.pt + i0;
-          const uint64_t w = __hip_atomic_load(const_cast<uint64_t*>(src + j), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-          if ((uint32_t)(w >> 32) == ep) pv[q][j] = __uint_as_float((uint32_t)w);
-          else still |= 1u << (4 * q + j);
-        }
-      }
-    }
-    pend = still;
   }
   // the world's sum in rank order (identical on every rank)
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
@@ -147,7 +152,7 @@ __global__ __launch_bounds__(64) void k_xchg_probe(const XchgDesc* xd, uint32_t 
     for (int q = 0; q < x.world; ++q) w += (float)((q + 1) * 4096) + base;
     want[j] = w;
   }
-  const f32x4 s = xchg_chunk(x, fault, g, x.pt - MDP_XCH_PROBE + p0, true, ep);
+  const f32x4 s = xchg_chunk(xd, fault, g, x.pt - MDP_XCH_PROBE + p0, true, ep);
   uint32_t nbad = 0;
   for (int j = 0; j < 4; ++j) nbad += s[j] != want[j] ? 1u : 0u;
   if (nbad) atomicAdd(bad, nbad);
@@ -222,7 +227,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       f32x4 g = red[0][col];
 #pragma unroll
       for (int q = 1; q < 16; ++q) g += red[q][col];
-      if (f.phase == 3) g = xchg_chunk(*f.xd, &a.ctl->fault, g, i0, act, ep);
+      if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ep);
       double ss = 0.0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
