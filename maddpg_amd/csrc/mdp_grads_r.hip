@@ -769,6 +769,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;
+  __shared__ int fwd_issued;  // waves 0..3 issued the loads the critic forward needs first
   int agent = a.agent, bx = blockIdx.x;
   if (a.cpre) {  // workgroups [B/16, 2 B/16): the next critic step's independent work (strict mode)
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
@@ -823,6 +824,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   double* slab_stat = a.slab_stat + ao * (int64_t)((a.B + MDP_R - 1) / MDP_R) * 8;
   MDP_STAMP(16);
   if (threadIdx.x == 0) rows_ready = 0;
+  if (threadIdx.x == 1) fwd_issued = 0;
   __syncthreads();  // B0
 
   if (wave < 4) {
@@ -830,26 +832,38 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       // ---------------- actor forward on obs_i -> logits p (maddpg.py:39), sample a_i (:49)
       f32x4 wda[4];
       float w3a[MDP_ACT_DIM];
+      float w2t[16];  // critic L2 column tile 0
+      float b2t, w3t;
       if (a.apre) {  // computed by the critic launch's extra workgroups: load the block
+        // issue order: the block (the sample a_i is on the path to B2), the
+        // critic L2 tile, then -- after fwd_issued -- the backward's weights
         const float* src = a.apre + (int64_t)r0 * MDP_APRE_W;
         f32x4 v[MDP_APRE_W / 16];
 #pragma unroll
         for (int k = 0; k < MDP_APRE_W / 16; ++k) v[k] = ld4(src + 4 * (lane + 64 * k));
+        rt_load<16>(w2t, P + nc.t[2].off, RH, r, RH);
+        b2t = P[nc.t[3].off + r];
+        w3t = P[nc.t[4].off + r];
+        lds_signal(&fwd_issued);
+        rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
+#pragma unroll
+        for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
 #pragma unroll
         for (int k = 0; k < MDP_APRE_W / 16; ++k)
           *reinterpret_cast<f32x4*>(apre_lds(lane + 64 * k, h1a, h2a, lg, av)) = v[k];
         wave_sync();
       } else {
+        lds_signal(&fwd_issued);
         actor_fwd_wave(P, na, ag, rowbuf, ldr, u_act, nvalid, r0, a.seed, agent, ctr, &rows_ready, 6, h1a, h2a, lg,
                        av);
-      }
-      // backward-phase weights: W1c rows of the a_i input (for da) and W3 of the actor (for d2a)
-      rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
+        // backward-phase weights: W1c rows of the a_i input (for da) and W3 of the actor (for d2a)
+        rdg_load(wda, P + nc.t[0].off + ag.a_in_off * RH, min(r, MDP_ACT_DIM - 1), r < MDP_ACT_DIM);
 #pragma unroll
-      for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
-      float w2t[16];  // critic L2 column tile 0
-      rt_load<16>(w2t, P + nc.t[2].off, RH, r, RH);
-      const float b2t = P[nc.t[3].off + r], w3t = P[nc.t[4].off + r];
+        for (int k = 0; k < MDP_ACT_DIM; ++k) w3a[k] = P[na.t[4].off + lane * MDP_ACT_DIM + k];
+        rt_load<16>(w2t, P + nc.t[2].off, RH, r, RH);
+        b2t = P[nc.t[3].off + r];
+        w3t = P[nc.t[4].off + r];
+      }
       MDP_STAMP(18);
       __syncthreads();  // B2: a_i and the L1 thirds ready
       __syncthreads();  // B2b: h1c ready
@@ -916,6 +930,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       float w2t[16];  // critic L2 column tile `wave`
       rt_load<16>(w2t, P + nc.t[2].off, RH, 16 * wave + r, RH);
       const float b2t = P[nc.t[3].off + 16 * wave + r], w3t = P[nc.t[4].off + 16 * wave + r];
+      lds_signal(&fwd_issued);
       lds_wait(&rows_ready, 6);
       if (wave == 1) MDP_STAMPW(56);
       f32x4 acc[4];
@@ -965,6 +980,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
     lds_signal(&rows_ready);
     f32x4 wc[4], wa[4];
+    lds_wait(&fwd_issued, 4);  // the critic forward's loads go first
     rdg_load(wc, P + nc.t[2].off, 16 * tt + r, true);
     rdg_load(wa, P + na.t[2].off, 16 * tt + r, true);
     __syncthreads();  // B2
