@@ -611,6 +611,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   float* da = cv.take(MDP_R * 8);
   float* dl = cv.take(MDP_R * 8);
   float* qv = cv.take(MDP_R * 8);
+  float* w1ai = cv.take(MDP_ACT_DIM * H);  // the critic's layer-1 rows of the a_i input (for da)
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = blockDim.x >> 6;
   const int r0 = blockIdx.x * MDP_R;
@@ -625,9 +626,12 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   const int cin = ag.cin;
 
   float pf[MDP_KC];  // this wave's next layer chunk, issued ahead (wave < NT)
+  MDP_STAMP(32);
   if (wave < NT) pf_load(pf, P + na.t[0].off, H, wave, 0, ag.obs_dim);
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
+  for (int e = tid; e < MDP_ACT_DIM * H; e += blockDim.x) w1ai[e] = P[nc.t[0].off + (int64_t)ag.a_in_off * H + e];
   __syncthreads();
+  MDP_STAMP(33);
   // actor forward on obs_i -> logits p (maddpg.py:39)
   if (wave < NT) {
     fwd_tile_pf<true>(rowbuf + ag.obs_off, ldr, 0, ag.obs_dim, P + na.t[0].off, P + na.t[1].off, H, nullptr, 0, h1a,
@@ -641,11 +645,13 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
     x[r * ldc + c] = rowbuf[r * ldr + src];
   }
   __syncthreads();
+  MDP_STAMP(34);
   if (wave < NT) {
     fwd_tile_pf<true>(h1a, ldh, 0, H, P + na.t[2].off, P + na.t[3].off, H, nullptr, 0, h2a, ldh, wave, pf);
     pf_load(pf, P + nc.t[0].off, H, wave, 0, cin);
   }
   __syncthreads();
+  MDP_STAMP(35);
   if (wave == 0) {
     head_mfma<H / 4>(h2a, ldh, H, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM, lg, 8);
     wave_sync();
@@ -662,17 +668,20 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
     }
   }
   __syncthreads();
+  MDP_STAMP(36);
   // critic (post-step weights) forward
   if (wave < NT) {
     fwd_tile_pf<true>(x, ldc, 0, cin, P + nc.t[0].off, P + nc.t[1].off, H, nullptr, 0, h1c, ldh, wave, pf);
     pf_load(pf, P + nc.t[2].off, H, wave, 0, H);
   }
   __syncthreads();
+  MDP_STAMP(37);
   if (wave < NT) {
     fwd_tile_pf<true>(h1c, ldh, 0, H, P + nc.t[2].off, P + nc.t[3].off, H, nullptr, 0, h2c, ldh, wave, pf);
     pf_load_t(pf, P + nc.t[2].off, H, wave);  // dh1c = d2 W2c^T
   }
   __syncthreads();
+  MDP_STAMP(38);
   // q (loss value, wave 0) ; dL/dq = -1/B ; d2 = dq * W3c masked by h2c > 0
   if (wave == 0) head_mfma<H / 4>(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
   const float* W3c = P + nc.t[4].off;
@@ -681,24 +690,30 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
     d2[r * ldh + h] = (r < nvalid && h2c[r * ldh + h] > 0.f) ? a.neg_inv_b * W3c[h] : 0.f;
   }
   __syncthreads();
+  MDP_STAMP(39);
   // dh1c = d2 @ W2c^T masked by h1c > 0
   if (wave < NT) {
     dgrad_tile_relu_pf(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh, wave, pf);
     pf_load_t(pf, P + na.t[2].off, H, wave);  // dh1a = d2a W2a^T, after the softmax backward
   }
   __syncthreads();
+  MDP_STAMP(56);
   if (wave == 0) {
-    // da[r][k] = sum_h d1[r][h] * W1c[a_in_off + k][h]   (only the a_i input columns)
+    // da[r][k] = sum_h d1[r][h] * W1c[a_in_off + k][h] (only the a_i input
+    // columns): one MFMA tile, column k < 5 of it, the W1c rows staged in LDS
+    // at the start.  (A VALU loop reading W1c from global memory took 14 us
+    // of the 45 us S5 actor step.)
     {
-      const float* W1c = P + nc.t[0].off + (int64_t)ag.a_in_off * H;
-      for (int base = 0; base < MDP_R * MDP_ACT_DIM; base += 16) {
-        const int o = base + (lane >> 2), q = lane & 3;
-        const int r = o / MDP_ACT_DIM, k = o - r * MDP_ACT_DIM;
-        float s = 0.f;
-        for (int h = q; h < H; h += 4) s = fmaf(d1[r * ldh + h], W1c[k * H + h], s);
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        if (q == 0) da[r * 8 + k] = s;
+      const int r = lane & 15, kq = lane >> 4, c = min(r, MDP_ACT_DIM - 1);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int s4 = 0; s4 < H / 4; ++s4) {
+        const int k = 4 * s4 + kq;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(d1[r * ldh + k], w1ai[c * H + k], acc, 0, 0, 0);
+      }
+      if (r < MDP_ACT_DIM) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) da[(kq * 4 + i) * 8 + r] = acc[i];
       }
     }
     wave_sync();
@@ -728,6 +743,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
     }
   }
   __syncthreads();
+  MDP_STAMP(57);
   // actor backward: dW3a, db3a, d2a = (dl @ W3a^T) masked by h2a > 0
   float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
   const float* W3a = P + na.t[4].off;
@@ -749,6 +765,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
     d2[r * ldh + h] = h2a[r * ldh + h] > 0.f ? s : 0.f;
   }
   __syncthreads();
+  MDP_STAMP(58);
   // dh1a tiles then dW2a tiles, dealt over all waves
   for (int t = wave; t < NT + NT * NT; t += nw) {
     if (t < NT) dgrad_tile_relu_pf(d2, ldh, H, P + na.t[2].off, h1a, ldh, d1, ldh, t, pf);
@@ -756,8 +773,10 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   }
   colsum16(d2, ldh, H, slab + na.t[3].off);
   __syncthreads();
+  MDP_STAMP(59);
   wgrad_waves(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1, ldh, H, slab + na.t[0].off, 0, nw);
   colsum16(d1, ldh, H, slab + na.t[1].off);
+  MDP_STAMP(60);
 }
 
 // ---------------------------------------------------------------- launchers

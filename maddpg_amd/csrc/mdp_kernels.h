@@ -257,7 +257,7 @@ inline int lds_critic_bytes(const Topo& t, int G) {
 }
 inline int lds_actor_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), S = R * (t.H + 1);
-  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(S) + 5 * mdp_r4(R * 8));
+  return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(S) + 5 * mdp_r4(R * 8) + mdp_r4(5 * t.H));
 }
 #define MDP_LDS_BUDGET (160 * 1024)
 // fast (register-resident, H = 64) variants in mdp_grads_r.hip

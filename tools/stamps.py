@@ -44,6 +44,15 @@ if not fast:
     print("per-wave layer-phase ends (us after the gather; L1 waves 0..15 | L2 waves 0..15):")
     print("  L1:", " ".join(f"{(st[16 + w] - st[1]) * 10 / 1000:5.2f}" for w in range(16)))
     print("  L2:", " ".join(f"{(st[40 + w] - st[6]) * 10 / 1000:5.2f}" for w in range(16)))
+    if st[32]:
+        anames = [(33, "gather"), (34, "actor L1"), (35, "actor L2"), (36, "head + Gumbel"), (37, "critic L1"),
+                  (38, "critic L2"), (39, "q, d2c"), (56, "dh1c"), (57, "da, softmax bwd"), (58, "dW3a, d2a"),
+                  (59, "dh1a, dW2a"), (60, "dW1a")]
+        print("general actor step (wave 0):")
+        prev = st[32]
+        for i, nm in anames:
+            print(f"{nm:>32s}: {(st[i] - prev) * 10 / 1000:7.2f} us  (t={(st[i] - st[32]) * 10 / 1000:6.2f})")
+            prev = st[i]
     seq = []
 else:
     names = {0: "start", 1: "B1 gather+weights (w0)", 2: "tgt actor fwd+gumbel (w0)", 3: "critic L1+L2 (w3)",
