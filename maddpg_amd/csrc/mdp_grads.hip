@@ -211,9 +211,28 @@ __device__ __forceinline__ void pf_load(float (&wa)[MDP_KC], const float* __rest
   const int lane = threadIdx.x & 63;
   load_wchunk(wa, W, N, nt * 16 + (lane & 15), k0, K, lane >> 4);
 }
-__device__ __forceinline__ void pf_load_t(float (&wa)[MDP_KC], const float* __restrict__ W, int N, int nt) {
+// Transposed operand of dX = dY @ W^T (W[K][N] row-major, N a multiple of 64):
+// output column kk = row kk of W, contraction order n = c0 + 16 kq + s within a
+// 64-deep chunk, so a lane's 16 fragments are 64 contiguous bytes of row kk --
+// four 16-B loads instead of sixteen strided 4-B ones (n = c0 + 4 s + kq)
+__device__ __forceinline__ void load_wchunk_tc(f32x4 (&w)[4], const float* __restrict__ W, int N, int kk, int c0,
+                                               int kq) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) w[m] = *reinterpret_cast<const f32x4*>(W + (int64_t)kk * N + c0 + 16 * kq + 4 * m);
+}
+__device__ __forceinline__ f32x4 mfma_chunk_tc(f32x4 acc, const f32x4 (&w)[4], const float* A, int lda, int r, int c0,
+                                               int kq) {
+  float x[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) x[q] = A[r * lda + c0 + 16 * kq + q];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[q], w[q >> 2][q & 3], acc, 0, 0, 0);
+  return acc;
+}
+__device__ __forceinline__ void pf_load_t(f32x4 (&wa)[4], const float* __restrict__ W, int N, int nt) {
   const int lane = threadIdx.x & 63;
-  load_wchunk_t(wa, W, N, nt * 16 + (lane & 15), 0, N, lane >> 4, true);
+  load_wchunk_tc(wa, W, N, nt * 16 + (lane & 15), 0, lane >> 4);
 }
 // Y tile = act([init +] X[:, k0:K] W[k0:K, :] + b); init (raw accumulator of the
 // rows before k0, same MFMA k order as one chain) may be null
@@ -246,21 +265,22 @@ __device__ __forceinline__ void fwd_tile_pf(const float* X, int ldx, int k0, int
     Y[(kq * 4 + i) * ldy + col] = v;
   }
 }
-// dX tile nt = (dY[16][N] @ W^T) masked by Hin > 0, first chunk of W^T in wa
+// dX tile nt = (dY[16][N] @ W^T) masked by Hin > 0 (N a multiple of 64), first
+// chunk of W^T in wa (pf_load_t); contiguous transposed fragments (load_wchunk_tc)
 __device__ __forceinline__ void dgrad_tile_relu_pf(const float* dY, int ldy, int N, const float* __restrict__ W,
                                                    const float* Hin, int ldh, float* dX, int ldx, int nt,
-                                                   float (&wa)[MDP_KC]) {
+                                                   f32x4 (&wa)[4]) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int kk = nt * 16 + r;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  float wb[MDP_KC];
-  for (int c0 = 0; c0 < N; c0 += 4 * MDP_KC) {
-    const bool more = c0 + 4 * MDP_KC < N;
-    if (more) load_wchunk_t(wb, W, N, kk, c0 + 4 * MDP_KC, N, kq, true);
-    acc = mfma_chunk(acc, wa, dY, ldy, r, c0, N, kq);
+  f32x4 wb[4];
+  for (int c0 = 0; c0 < N; c0 += 64) {
+    const bool more = c0 + 64 < N;
+    if (more) load_wchunk_tc(wb, W, N, kk, c0 + 64, kq);
+    acc = mfma_chunk_tc(acc, wa, dY, ldy, r, c0, kq);
     if (more) {
 #pragma unroll
-      for (int s = 0; s < MDP_KC; ++s) wa[s] = wb[s];
+      for (int m = 0; m < 4; ++m) wa[m] = wb[m];
     }
   }
 #pragma unroll
@@ -350,6 +370,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   float* h2c = hB + G * S;
   float* qv = lg + G * MDP_R * 8;
   float pf[MDP_KC];  // this wave's next single-net layer chunk, issued ahead (wave < NT)
+  f32x4 pft[4];      // the backward's first W^T chunk, issued ahead
   MDP_STAMP(0);
 
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
@@ -516,7 +537,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     __syncthreads();
     if (wave < NT) {
       fwd_tile_pf<true>(hA, ldh, 0, H, P + nd.t[2].off, P + nd.t[3].off, H, nullptr, 0, hB, ldh, wave, pf);
-      pf_load_t(pf, a.theta + nd.t[2].off, H, wave);  // the backward's dh1 = d2 W2^T
+      pf_load_t(pft, a.theta + nd.t[2].off, H, wave);  // the backward's dh1 = d2 W2^T
     }
     __syncthreads();
   }
@@ -579,7 +600,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   MDP_STAMP(4);
   // dh1 tiles then dW2 tiles, dealt over all waves
   for (int t = wave; t < NT + NT * NT; t += nw) {
-    if (t < NT) dgrad_tile_relu_pf(d2, ldh, H, a.theta + nd.t[2].off, h1c, ldh, d1, ldh, t, pf);
+    if (t < NT) dgrad_tile_relu_pf(d2, ldh, H, a.theta + nd.t[2].off, h1c, ldh, d1, ldh, t, pft);
     else wgrad_tile(h1c, ldh, H, d2, ldh, H, slab + nd.t[2].off, t - NT);
   }
   colsum16(d2, ldh, H, slab + nd.t[3].off);
@@ -626,6 +647,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   const int cin = ag.cin;
 
   float pf[MDP_KC];  // this wave's next layer chunk, issued ahead (wave < NT)
+  f32x4 pft[4];      // the next transposed (backward) chunk, issued ahead
   MDP_STAMP(32);
   if (wave < NT) pf_load(pf, P + na.t[0].off, H, wave, 0, ag.obs_dim);
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
@@ -678,7 +700,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   MDP_STAMP(37);
   if (wave < NT) {
     fwd_tile_pf<true>(h1c, ldh, 0, H, P + nc.t[2].off, P + nc.t[3].off, H, nullptr, 0, h2c, ldh, wave, pf);
-    pf_load_t(pf, P + nc.t[2].off, H, wave);  // dh1c = d2 W2c^T
+    pf_load_t(pft, P + nc.t[2].off, H, wave);  // dh1c = d2 W2c^T
   }
   __syncthreads();
   MDP_STAMP(38);
@@ -693,8 +715,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   MDP_STAMP(39);
   // dh1c = d2 @ W2c^T masked by h1c > 0
   if (wave < NT) {
-    dgrad_tile_relu_pf(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh, wave, pf);
-    pf_load_t(pf, P + na.t[2].off, H, wave);  // dh1a = d2a W2a^T, after the softmax backward
+    dgrad_tile_relu_pf(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh, wave, pft);
+    pf_load_t(pft, P + na.t[2].off, H, wave);  // dh1a = d2a W2a^T, after the softmax backward
   }
   __syncthreads();
   MDP_STAMP(56);
@@ -768,7 +790,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   MDP_STAMP(58);
   // dh1a tiles then dW2a tiles, dealt over all waves
   for (int t = wave; t < NT + NT * NT; t += nw) {
-    if (t < NT) dgrad_tile_relu_pf(d2, ldh, H, P + na.t[2].off, h1a, ldh, d1, ldh, t, pf);
+    if (t < NT) dgrad_tile_relu_pf(d2, ldh, H, P + na.t[2].off, h1a, ldh, d1, ldh, t, pft);
     else wgrad_tile(h1a, ldh, H, d2, ldh, H, slab + na.t[2].off, t - NT);
   }
   colsum16(d2, ldh, H, slab + na.t[3].off);
