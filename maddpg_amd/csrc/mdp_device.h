@@ -297,6 +297,34 @@ __device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const 
   }
 }
 
+// head_mfma in two steps, so the head's weight fragments can be issued ahead
+// (K = 4 KS; columns r >= nout are computed but never stored, so the loads need
+// no select -- a select on the loaded value would wait for it at the load)
+template <int KS>
+__device__ __forceinline__ void head_load(float (&w)[KS], float& bias, const float* __restrict__ W,
+                                          const float* __restrict__ b, int nout) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  const int c = min(r, nout - 1);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) w[s] = W[(4 * s + kq) * nout + c];
+  bias = b[c];
+}
+template <int KS>
+__device__ __forceinline__ void head_acc(const float (&w)[KS], float bias, const float* X, int ldx, int nout,
+                                         float* out, int ldo) {
+  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
+  float x[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) x[s] = X[r * ldx + 4 * s + kq];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+  if (r < nout) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(kq * 4 + i) * ldo + r] = acc[i] + bias;
+  }
+}
+
 // out[16][nout] = X[16][K] @ W[K][nout] + b  (small heads, VALU; 4 lanes per output)
 __device__ __forceinline__ void tile_head(const float* X, int ldx, int K, const float* __restrict__ W,
                                  const float* __restrict__ b, int nout, float* out, int ldo) {

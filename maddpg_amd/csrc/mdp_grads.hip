@@ -668,6 +668,10 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   }
   __syncthreads();
   MDP_STAMP(34);
+  // the actor head's fragments (wave 0), issued ahead of the layer-2 tile
+  constexpr int HKS = H / 4 <= 32 ? H / 4 : 1;
+  float hw[HKS], hb = 0.f;
+  if (H / 4 <= 32 && wave == 0) head_load<HKS>(hw, hb, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM);
   if (wave < NT) {
     fwd_tile_pf<true>(h1a, ldh, 0, H, P + na.t[2].off, P + na.t[3].off, H, nullptr, 0, h2a, ldh, wave, pf);
     pf_load(pf, P + nc.t[0].off, H, wave, 0, cin);
@@ -675,7 +679,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   __syncthreads();
   MDP_STAMP(35);
   if (wave == 0) {
-    head_mfma<H / 4>(h2a, ldh, H, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM, lg, 8);
+    if constexpr (H / 4 <= 32) head_acc<HKS>(hw, hb, h2a, ldh, MDP_ACT_DIM, lg, 8);
+    else head_mfma<H / 4>(h2a, ldh, H, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM, lg, 8);
     wave_sync();
     if (lane < MDP_R) {  // fresh Gumbel sample (maddpg.py:49)
       float u[MDP_ACT_DIM];
@@ -698,14 +703,19 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   }
   __syncthreads();
   MDP_STAMP(37);
+  float qw[HKS], qb = 0.f;  // the critic head's fragments (q), issued ahead on an idle wave
   if (wave < NT) {
     fwd_tile_pf<true>(h1c, ldh, 0, H, P + nc.t[2].off, P + nc.t[3].off, H, nullptr, 0, h2c, ldh, wave, pf);
     pf_load_t(pft, P + nc.t[2].off, H, wave);  // dh1c = d2 W2c^T
+  } else if (H / 4 <= 32 && wave == nw - 1) {
+    head_load<HKS>(qw, qb, P + nc.t[4].off, P + nc.t[5].off, 1);
   }
   __syncthreads();
   MDP_STAMP(38);
-  // q (loss value, wave 0) ; dL/dq = -1/B ; d2 = dq * W3c masked by h2c > 0
-  if (wave == 0) head_mfma<H / 4>(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
+  // dL/dq = -1/B ; d2 = dq * W3c masked by h2c > 0.  q (the loss value only)
+  // waits for the next phase, on a wave the dh1c tiles leave idle
+  const bool q_late = NT < nw;
+  if (!q_late && wave == 0) head_mfma<H / 4>(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
   const float* W3c = P + nc.t[4].off;
   for (int e = tid; e < MDP_R * H; e += blockDim.x) {
     const int r = e / H, h = e - r * H;
@@ -717,6 +727,9 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   if (wave < NT) {
     dgrad_tile_relu_pf(d2, ldh, H, P + nc.t[2].off, h1c, ldh, d1, ldh, wave, pft);
     pf_load_t(pft, P + na.t[2].off, H, wave);  // dh1a = d2a W2a^T, after the softmax backward
+  } else if (q_late && wave == nw - 1) {
+    if constexpr (H / 4 <= 32) head_acc<HKS>(qw, qb, h2c, ldh, 1, qv, 8);
+    else head_mfma<H / 4>(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
   }
   __syncthreads();
   MDP_STAMP(56);
