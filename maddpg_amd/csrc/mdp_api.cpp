@@ -206,7 +206,9 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   // computes every agent's gradients in one launch; strict mode uses block 0)
   sz[MDP_R_SLAB] = (int64_t)n * (4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg +
                                   8 * (int64_t)c->batch_size) + 256 + 256 + mdp_ra_sync_bytes() +
-                   4 * (int64_t)L.nwg * 16 * (MDP_APRE_W + MDP_CPRE_W + 2 * T.row_stride);  // precomputed work + rows
+                   4 * (int64_t)L.nwg * 16 * (MDP_APRE_W + MDP_CPRE_W + 2 * T.row_stride) +  // precomputed work + rows
+                   4 * (int64_t)mdp_pair_rows(c->batch_size) * MDP_ACT_DIM * n + 8 * (int64_t)n * L.nwg +
+                   512;  // pair hand-off (whole pairs of rows) + counters
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
   for (int r = 0; r < MDP_R_COUNT; ++r) {
@@ -298,6 +300,12 @@ struct mdp_handle {
   bool critic_pre = true;
   float* apre_rows = nullptr;  // the replay rows those launches gathered (read contiguously by the step)
   float* cpre_rows = nullptr;
+  // general critic step as pairs of workgroups per 32 rows (mdp_grads_pair.hip),
+  // opt-in with MDP_PAIR=1 (measured slower than k_critic_grad at S5: DESIGN §4)
+  bool pair_mode = false;
+  float* pair_xa = nullptr;
+  uint32_t* pair_prod = nullptr;
+  uint32_t* pair_cons = nullptr;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
   // mdp_train_step graphs (rollout + k rounds), one per k
@@ -445,6 +453,34 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
   return 0;
 }
 
+bool tp_fast(const mdp_handle* h);
+
+// which critic kernel serves agent `agent`: the fast register-resident one
+// (strict order, H = 64 topologies), else the general one -- as the pair kernel
+// (MADDPG critics, H <= 128, its LDS fits) with MDP_PAIR=1
+bool crit_general(const mdp_handle* h, int agent, bool tp) {
+  return tp ? !tp_fast(h) : (h->general_grads || !grads_r_ok(h->L.topo, agent));
+}
+// target actors per pass of the pair kernel's actor workgroup: the fewest
+// passes the LDS budget allows, the actors spread evenly over them (0: none fit)
+int pair_group(const Topo& T) {
+  int G = T.n;
+  while (G > 0 && lds_pair_bytes(T, G) > MDP_LDS_BUDGET) --G;
+  if (G == 0) return 0;
+  const int passes = (T.n + G - 1) / G;
+  return (T.n + passes - 1) / passes;
+}
+bool pair_ok(const mdp_handle* h, int agent, bool tp) {
+  const Topo& T = h->L.topo;
+  return h->pair_mode && crit_general(h, agent, tp) && !T.ag[agent].local_q && (T.H == 64 || T.H == 128) &&
+         pair_group(T) > 0;
+}
+// partial-gradient slabs the critic step of `agent` leaves: one per 16 rows,
+// one per 32 with the pair kernel
+int crit_nwg(const mdp_handle* h, int agent, bool tp) {
+  return pair_ok(h, agent, tp) ? (h->cfg.batch_size + MDP_PAIR_R - 1) / MDP_PAIR_R : h->L.nwg;
+}
+
 // tp: throughput mode on the general kernels -- this agent's own blocks of
 // partials / stats / TD targets and noise counter upd_ctr + agent (multi = 2
 // marks it; the general kernels take the agent from a.agent, not the grid)
@@ -457,6 +493,8 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.cpre_rows = h->cpre_rows;
   a.apre_rows = h->apre_rows;
   a.cpre_prev = post_prev;
+  a.pair_xa = nullptr;
+  a.pair_prod = a.pair_cons = nullptr;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.pf_ctl = h->ctl;
@@ -492,6 +530,15 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
     if (apre) a.apre = h->apre;
     if (post_prev >= 0) a.cpre = h->cpre;
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
+    return 0;
+  }
+  if (pair_ok(h, agent, tp)) {
+    const Topo& T = h->L.topo;
+    a.group = pair_group(T);
+    a.pair_xa = h->pair_xa;
+    a.pair_prod = h->pair_prod + (int64_t)agent * h->L.nwg;
+    a.pair_cons = h->pair_cons + (int64_t)agent * h->L.nwg;
+    HIPCHK(h, mdp_launch_critic_pair(a, T.H, lds_pair_bytes(T, a.group), h->stream));
     return 0;
   }
   // as many target actors per pass as the LDS budget allows (all of them for S1-S4)
@@ -549,7 +596,7 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
 }
 
 // net 1: critic Adam (+ critic stats); net 0: actor Adam + Polyak of both nets (+ actor stats)
-ApplyArgs apply_args(mdp_handle* h, int agent, int net, float scale) {
+ApplyArgs apply_args(mdp_handle* h, int agent, int net, float scale, bool tp = false) {
   const ADesc& ag = h->L.topo.ag[agent];
   ApplyArgs a;
   a.net = net ? ag.critic : ag.actor;
@@ -568,7 +615,7 @@ ApplyArgs apply_args(mdp_handle* h, int agent, int net, float scale) {
   chunks(a.other, a.oblk);
   a.slab = nullptr;
   a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
-  a.nwg = h->L.nwg;
+  a.nwg = net ? crit_nwg(h, agent, tp) : h->L.nwg;
   a.scale = scale;
   a.clip = h->cfg.grad_clip;
   a.lr = h->cfg.lr;
@@ -610,9 +657,9 @@ bool reduce_apply_ok(const mdp_handle* h, int agent, int net) {
   return mdp_ra_fits(h->L.topo, agent, net, h->ra_cap);
 }
 
-FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net) {
+FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net, bool tp = false) {
   FusedApplyArgs f;
-  f.ap = apply_args(h, agent, net, 1.0f);
+  f.ap = apply_args(h, agent, net, 1.0f, tp);
   f.ap.slab = net ? h->slab_c : h->slab_a;
   f.rblk[0] = 0;
   for (int t = 0; t < 6; ++t)
@@ -672,7 +719,7 @@ int do_reduce(mdp_handle* h, int agent, int net) {
   const NDesc& d = net_of(h, agent, net);
   ReduceArgs a;
   a.slab = net ? h->slab_c : h->slab_a;
-  a.nwg = h->L.nwg;
+  a.nwg = net ? crit_nwg(h, agent, false) : h->L.nwg;
   a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
   a.grad = h->grad;
   a.off = d.off;
@@ -837,7 +884,7 @@ bool tp_ok(const mdp_handle* h) {
 // upd_ctr + agent)
 FusedApplyArgs tp_args(mdp_handle* h, int agent, int net) {
   const int64_t nwg = h->L.nwg;
-  FusedApplyArgs f = fused_args_for(h, agent, net);
+  FusedApplyArgs f = fused_args_for(h, agent, net, true);
   f.ap.slab = net ? h->slab_c + agent * nwg * h->L.slab_c : h->slab_a + agent * nwg * h->L.slab_a;
   f.ap.slab_stat = (net ? h->stat_c : h->stat_a) + agent * nwg * 8;
   f.ap.y = h->y + (int64_t)agent * h->cfg.batch_size;
@@ -906,6 +953,8 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
     a.cpre = nullptr;
     a.cpre_rows = nullptr;
     a.cpre_prev = -1;
+    a.pair_xa = nullptr;
+    a.pair_prod = a.pair_cons = nullptr;
     a.pf_ctl = h->ctl;
     a.pf_out = pf_out;
     a.pf_count = pf_out ? n * h->cfg.batch_size : 0;
@@ -1072,6 +1121,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->actor_pre = !(ap && ap[0] == '0');
     const char* cp = getenv("MDP_CRITIC_PRE");
     h->critic_pre = !(cp && cp[0] == '0');
+    const char* pm = getenv("MDP_PAIR");
+    h->pair_mode = pm && pm[0] == '1';
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
@@ -1142,6 +1193,10 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->cpre = h->apre + (int64_t)nwg * 16 * MDP_APRE_W;
     h->apre_rows = h->cpre + (int64_t)nwg * 16 * MDP_CPRE_W;
     h->cpre_rows = h->apre_rows + (int64_t)nwg * 16 * h->L.topo.row_stride;
+    h->pair_xa = h->cpre_rows + (int64_t)nwg * 16 * h->L.topo.row_stride;
+    h->pair_prod = (uint32_t*)(((uintptr_t)(h->pair_xa + mdp_pair_rows(cfg->batch_size) * MDP_ACT_DIM * na) + 255) &
+                               ~uintptr_t(255));
+    h->pair_cons = h->pair_prod + na * nwg;
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
   std::vector<float> beta(8 * cfg->n_agents);

@@ -113,38 +113,54 @@ __device__ __forceinline__ void rg_acc(f32x4 (&acc)[4], const float* X, int ldx,
     }
   }
 }
+// The chunks ping-pong between two register sets with the loop unrolled by
+// two: the next chunk's loads are issued before the wait for the current one,
+// so two chunks are in flight during a wait, and the compiler waits for exactly
+// the chunk it is about to use.  (A copy wa = wb of the prefetch buffer at the
+// end of each iteration made the wave wait there for every load in flight:
+// one chunk in flight at a time.)  Each chunk load also fetches the unit's
+// bias, so the store at a unit's end does not wait behind the prefetch.
 template <class JobFn>
 __device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, int ldy, JobFn job) {
   constexpr int KS = MDP_GKS;  // k-steps (of 4) per chunk
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
   const int r = lane & 15, kq = lane >> 4, ngr = N >> 6, total = njobs * ngr;
-  int u = wave;
-  if (u >= total) return;
-  TileJob j = job(u / ngr);
-  int g = u % ngr, c0 = j.k0;
-  f32x4 wa[KS], wb[KS];
-  rg_load<KS>(wa, j.W, N, 64 * g + 4 * r, c0, j.K, kq);
+  struct It {
+    int u, g, c0;
+    TileJob j;
+  };
+  It a;
+  a.u = wave;
+  if (a.u >= total) return;
+  a.j = job(a.u / ngr);
+  a.g = a.u % ngr;
+  a.c0 = a.j.k0;
+  auto next = [&](It& it) -> bool {
+    const int c2 = it.c0 + 4 * KS;
+    if (c2 < it.j.K) {
+      it.c0 = c2;
+      return true;
+    }
+    it.u += nw;
+    if (it.u >= total) return false;
+    it.j = job(it.u / ngr);
+    it.g = it.u % ngr;
+    it.c0 = it.j.k0;
+    return true;
+  };
+  f32x4 wa[KS], wb[KS], ba = {0.f, 0.f, 0.f, 0.f}, bb = ba;
+  auto load = [&](f32x4(&w)[KS], f32x4& bias, const It& it) {
+    rg_load<KS>(w, it.j.W, N, 64 * it.g + 4 * r, it.c0, it.j.K, kq);
+    if (it.j.b) bias = *reinterpret_cast<const f32x4*>(it.j.b + 64 * it.g + 4 * r);
+  };
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  while (true) {
-    int u2 = u, c2 = c0 + 4 * KS, g2 = g;
-    TileJob j2 = j;
-    if (c2 >= j.K) {  // next unit of this wave
-      u2 = u + nw;
-      if (u2 < total) {
-        j2 = job(u2 / ngr);
-        g2 = u2 % ngr;
-        c2 = j2.k0;
-      }
-    }
-    const bool more = u2 < total;
-    if (more) rg_load<KS>(wb, j2.W, N, 64 * g2 + 4 * r, c2, j2.K, kq);
-    rg_acc<KS>(acc, lds + j.xoff, j.ldx, r, c0, j.K, kq, wa);
-    if (c0 + 4 * KS >= j.K) {  // unit done: bias, ReLU, scatter the 4 tiles' columns
-      float* Y = lds + j.yoff + 64 * g + 4 * r;
-      if (j.b) {
-        const f32x4 bias = *reinterpret_cast<const f32x4*>(j.b + 64 * g + 4 * r);
+  auto step = [&](const It& it, const f32x4(&w)[KS], const f32x4& bias) {
+    rg_acc<KS>(acc, lds + it.j.xoff, it.j.ldx, r, it.c0, it.j.K, kq, w);
+    if (it.c0 + 4 * KS >= it.j.K) {  // unit done: bias, ReLU, scatter the 4 tiles' columns
+      float* Y = lds + it.j.yoff + 64 * it.g + 4 * r;
+      if (it.j.b) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -160,13 +176,118 @@ __device__ __forceinline__ void fwd_phase_grouped(float* lds, int njobs, int N, 
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if (!more) break;
+  };
+  load(wa, ba, a);
+  while (true) {
+    It b = a;
+    const bool hb = next(b);
+    if (hb) load(wb, bb, b);
+    step(a, wa, ba);
+    if (!hb) break;
+    It c = b;
+    const bool hc = next(c);
+    if (hc) load(wa, ba, c);
+    step(b, wb, bb);
+    if (!hc) break;
+    a = c;
+  }
+}
+
+// Layer 1 and layer 2 of independent nets as ONE phase fed by a work queue.
+// Waves take 64-column units from an LDS counter in the order
+//   layer 1 of the long jobs (listed first by the caller: the critic, K = cin,
+//   and the target critic's obs' part, K = sum_obs), layer 1 of the target
+//   actors, layer 2 of the target actors, layer 2 of the critic,
+// and a layer-2 unit of net q waits only for net q's layer-1 units (cnt[q]
+// reaches `want`), not for a workgroup barrier.  Stamped at tag N=6, H=128:
+// with the two layers as separate barrier phases, 12 waves finished layer 1 at
+// ~3.5 us while the long chains ran to 8.4 us; with a static deal of the fused
+// phase the waves holding the long chains still carried 9 of the 88 chunks
+// (5.5 per wave on average) -- every chunk costs ~2 us once all 16 waves
+// stream (the per-CU weight-stream ceiling), so the phase is set by the most
+// loaded wave.  No deadlock: layer-1 units wait for nothing and every one is
+// taken before any layer-2 unit.  job(layer, j) -> TileJob; L1 job j1(q) and
+// net index net1(q) come from the caller's order.  Ping-pong chunk stream as
+// fwd_phase_grouped.
+template <class JobFn, class OrdFn>
+__device__ __forceinline__ void fwd_phase_l12(float* lds, int nj1, int nj2, int N, int ldy, int* cnt, int* qctr,
+                                              int want, JobFn job, OrdFn ord) {
+  constexpr int KS = MDP_GKS;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, kq = lane >> 4, ngr = N >> 6, t1 = nj1 * ngr, tot = t1 + nj2 * ngr;
+  struct It {
+    int layer, net, g, c0;
+    TileJob j;
+  };
+  // next unit from the queue (one LDS atomic per unit, lane 0, broadcast)
+  auto take = [&](It& it) -> bool {
+    int q = 0;
+    if (lane == 0) q = __hip_atomic_fetch_add(qctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    q = __builtin_amdgcn_readfirstlane(q);
+    if (q >= tot) return false;
+    it.layer = q < t1 ? 0 : 1;
+    const int qq = q < t1 ? q : q - t1;
+    const int jb = it.layer == 0 ? ord(qq / ngr) : qq / ngr;  // layer 2: the caller's job order (actors, critic)
+    it.net = jb;
+    it.j = job(it.layer, jb);
+    it.g = qq % ngr;
+    it.c0 = it.j.k0;
+    return true;
+  };
+  auto next = [&](It& it) -> bool {
+    const int c2 = it.c0 + 4 * KS;
+    if (c2 < it.j.K) {
+      it.c0 = c2;
+      return true;
+    }
+    return take(it);
+  };
+  It a;
+  if (!take(a)) return;
+  f32x4 wa[KS], wb[KS], ba = {0.f, 0.f, 0.f, 0.f}, bb = ba;
+  auto load = [&](f32x4(&w)[KS], f32x4& bias, const It& it) {
+    rg_load<KS>(w, it.j.W, N, 64 * it.g + 4 * r, it.c0, it.j.K, kq);
+    if (it.j.b) bias = *reinterpret_cast<const f32x4*>(it.j.b + 64 * it.g + 4 * r);
+  };
+  f32x4 acc[4];
 #pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) wa[s2] = wb[s2];
-    u = u2;
-    c0 = c2;
-    g = g2;
-    j = j2;
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto step = [&](const It& it, const f32x4(&w)[KS], const f32x4& bias) {
+    if (it.layer == 1 && it.c0 == it.j.k0) lds_wait(cnt + it.net, want);
+    rg_acc<KS>(acc, lds + it.j.xoff, it.j.ldx, r, it.c0, it.j.K, kq, w);
+    if (it.c0 + 4 * KS >= it.j.K) {  // unit done: bias, ReLU, scatter the 4 tiles' columns
+      float* Y = lds + it.j.yoff + 64 * it.g + 4 * r;
+      if (it.j.b) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) Y[(kq * 4 + i) * ldy + t] = fmaxf(acc[t][i] + bias[t], 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) Y[(kq * 4 + i) * ldy + t] = acc[t][i];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (it.layer == 0) lds_signal(cnt + it.net);
+    }
+  };
+  load(wa, ba, a);
+  while (true) {
+    It b = a;
+    const bool hb = next(b);
+    if (hb) load(wb, bb, b);
+    step(a, wa, ba);
+    if (!hb) break;
+    It c = b;
+    const bool hc = next(c);
+    if (hc) load(wa, ba, c);
+    step(b, wb, bb);
+    if (!hc) break;
+    a = c;
   }
 }
 
@@ -357,6 +478,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   float* hB = cv.take((G + 1) * S);
   float* lg = cv.take((G + 1) * MDP_R * 8);
   float* dq = cv.take(MDP_R);
+  int* cnt = reinterpret_cast<int*>(cv.take(MDP_MAX_AGENTS + 4));  // layer-1 units done per net, then the
+                                                                    // work-queue counter (fwd_phase_l12)
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = blockDim.x >> 6;
   const int r0 = blockIdx.x * MDP_R;
@@ -383,6 +506,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   } else {
     copy_cols16(rowbuf, ldr, T.ag[0].nobs_off, xt, ldc, 0, T.sum_obs);
   }
+  if (tid < MDP_MAX_AGENTS + 4) cnt[tid] = 0;
   __syncthreads();
   const float* Xc = lq ? xl : rowbuf;  // critic input: the row prefix (global) or [obs_i | act_i]
   const int ldX = lq ? ldc : ldr;
@@ -423,8 +547,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     const bool sp = split && g0 == 0;
     const int nj1 = sp ? sc + st + ng : nj + (g0 == 0 && tpre ? 1 : 0);  // layer-1 jobs
     const int o_row = (int)(rowbuf - lds), o_xc = (int)(Xc - lds), o_ha = (int)(hA - lds), o_hb = (int)(hB - lds);
-    for (int layer = 0; layer < 2; ++layer) {
-      fwd_phase_grouped(lds, layer == 0 ? nj1 : nj, H, ldh, [&](int jb) {
+    auto jobf = [&](int layer, int jb) -> TileJob {
         if (sp && layer == 0 && jb < sc + st) {  // a split-K slice, raw into hB slot jb
           const bool crit = jb < sc;
           const int q = crit ? jb : jb - sc, ns = crit ? sc : st;
@@ -474,7 +597,22 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
           j.yoff = o_hb + slot;
         }
         return j;
-      });
+    };
+    if (!sp && H >= 128) {  // layer 1 + layer 2 as one phase, per-net hand-off (fwd_phase_l12; at H = 64 it spills)
+      // layer-1 order: the long jobs first (critic, the target critic's obs' part), then the actors
+      const int nlong = nj1 - ng;
+      fwd_phase_l12(lds, nj1, nj, H, ldh, cnt, cnt + MDP_MAX_AGENTS + 3, (H >> 6) * (g0 / G + 1), jobf,
+                    [&](int q) { return q < nlong ? ng + q : q - nlong; });
+      if (g0 == 0) MDP_STAMPW(16 + wave);  // per-wave phase end (diagnostic build)
+      __syncthreads();
+      if (tid == 0) cnt[MDP_MAX_AGENTS + 3] = 0;  // the queue of the next group (barriers follow)
+      if (g0 == 0) {
+        MDP_STAMP(6);
+        MDP_STAMP(7);
+      }
+    } else {
+    for (int layer = 0; layer < 2; ++layer) {
+      fwd_phase_grouped(lds, layer == 0 ? nj1 : nj, H, ldh, [&](int jb) { return jobf(layer, jb); });
       if (g0 == 0) MDP_STAMPW((layer == 0 ? 16 : 40) + wave);  // per-wave phase end (diagnostic build)
       __syncthreads();
       if (sp && layer == 0) {  // sum the slices in slice order: critic h1 = relu(sum + b1), obs' part raw
@@ -493,6 +631,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
         __syncthreads();
       }
       if (g0 == 0) MDP_STAMP(6 + layer);
+    }
     }
     // heads: net jb on wave jb % nw, then the Gumbel-softmax target actions
     for (int jb = wave; jb < nj; jb += nw) {

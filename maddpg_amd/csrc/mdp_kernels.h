@@ -48,6 +48,13 @@ struct CriticArgs {
   const float* cpre;
   const float* cpre_rows;  // the replay rows the critic_pre gathered, [B][row_stride]
   int cpre_prev;
+  // k_critic_pair (general kernels, MADDPG critics): per 32 batch rows a pair
+  // of workgroups -- the target actors' workgroup hands the target actions a~
+  // over through pair_xa [B][5 n] and bumps pair_prod[p]; the critic's
+  // workgroup waits until pair_prod[p] passes its own count pair_cons[p]
+  float* pair_xa;
+  uint32_t* pair_prod;
+  uint32_t* pair_cons;
 };
 
 // precomputed critic-step work of one batch row (k_actor_grad_r's extra
@@ -253,13 +260,31 @@ inline int mdp_ld(int c) { return c | 1; }
 inline int lds_critic_bytes(const Topo& t, int G) {
   const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), S = R * (t.H + 1);
   return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldc) + 2 * mdp_r4((G + 1) * S) + mdp_r4((G + 1) * R * 8) +
-              mdp_r4(R));
+              mdp_r4(R) + mdp_r4(MDP_MAX_AGENTS + 4));
 }
 inline int lds_actor_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), ldc = mdp_ld(t.cin_max), S = R * (t.H + 1);
   return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(S) + 5 * mdp_r4(R * 8) + mdp_r4(5 * t.H));
 }
 #define MDP_LDS_BUDGET (160 * 1024)
+// paired general critic step (mdp_grads_pair.hip): 32 rows per pair; the
+// target-actor workgroup holds obs' and G actors' h1/h2/logits, the critic
+// workgroup the rows, h1/h2 of the critic, the target critic's obs' partial,
+// its h1/h2 (then the deltas) and the target actions
+#define MDP_PAIR_R 32
+inline int64_t mdp_pair_rows(int64_t B) { return (B + MDP_PAIR_R - 1) / MDP_PAIR_R * MDP_PAIR_R; }
+inline int lds_pair_a_bytes(const Topo& t, int G) {
+  const int R = MDP_PAIR_R, ldo = mdp_ld(t.sum_obs + 4), S = R * (t.H + 1);
+  return 4 * (mdp_r4(R * ldo) + 2 * G * mdp_r4(S) + mdp_r4(G * R * 8));
+}
+inline int lds_pair_b_bytes(const Topo& t) {
+  const int R = MDP_PAIR_R, ldr = mdp_ld(t.row_stride), S = R * (t.H + 1), ldx = mdp_ld(5 * t.n);
+  return 4 * (mdp_r4(R * ldr) + 5 * mdp_r4(S) + mdp_r4(R * ldx) + 3 * mdp_r4(R * 8) + mdp_r4(R));
+}
+inline int lds_pair_bytes(const Topo& t, int G) {
+  const int a = lds_pair_a_bytes(t, G), b = lds_pair_b_bytes(t);
+  return a > b ? a : b;
+}
 // fast (register-resident, H = 64) variants in mdp_grads_r.hip
 inline int lds_critic_r_bytes(const Topo& t, int agent) {
   const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, LD = 65;
@@ -298,6 +323,8 @@ inline int lds_eval_bytes(int in, int H) {
 }
 
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
+// paired general critic step: grid 2 ceil(B / 32), a.group target actors per pass
+hipError_t mdp_launch_critic_pair(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s);

@@ -247,11 +247,30 @@ def test_update_parity_tag4_h64_general_kernels():
     _update_parity([16, 16, 16, 14], B=512, L=2000, seed=26)
 
 
+@pytest.mark.parametrize("pair", ["1", "0"])
 @pytest.mark.parametrize("local_q", [None, [True, False, False]])
-def test_update_parity_general_kernels_forced(monkeypatch, local_q):
-    # the general kernels (mdp_grads.hip) on a configuration the fast ones also serve
+def test_update_parity_general_kernels_forced(monkeypatch, local_q, pair):
+    # the general kernels (mdp_grads.hip) on a configuration the fast ones also
+    # serve; MADDPG critics on the pair kernel (mdp_grads_pair.hip) or, with
+    # MDP_PAIR=0, the single-workgroup one
     monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
+    monkeypatch.setenv("MDP_PAIR", pair)
     _update_parity([18, 18, 18], B=256, L=1200, seed=27, local_q=local_q)
+
+
+def test_update_parity_pair_ragged_batch(monkeypatch):
+    # the pair kernel's last pair only partly filled (B = 200: 6 pairs + 8 rows)
+    monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
+    monkeypatch.setenv("MDP_PAIR", "1")
+    _update_parity([18, 18, 18], B=200, L=900, seed=31)
+
+
+@pytest.mark.parametrize("pair", ["1", "0"])
+def test_update_parity_tag6_h128_ragged(monkeypatch, pair):
+    # tag N=6 at H=128, B = 1000: the pair kernel (31 pairs + 8 rows) and the
+    # single-workgroup kernel's work-queue layer phase (62 row tiles + 8 rows)
+    monkeypatch.setenv("MDP_PAIR", pair)
+    _update_parity([22, 22, 22, 22, 20, 20], B=1000, L=6000, seed=32, H=128)
 
 
 @pytest.mark.parametrize("dims,local_q,B,H", [([18, 18, 18], None, 1024, 64),
