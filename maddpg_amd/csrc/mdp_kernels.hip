@@ -704,12 +704,14 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   float* sv = cv.take(MDP_R * 2 * MDP_MAX_ENT);
 
   const int tid = threadIdx.x;
-  const int e0 = blockIdx.x * MDP_R;
+  // with a draw workgroup it is block 0 (dispatched first: at tag6 B=4096 the
+  // draw is 24,576 indices) and the env copies start at block 1
+  const int e0 = ((int)blockIdx.x - (a.pf_count > 0 ? 1 : 0)) * MDP_R;
   const int nvalid = min(MDP_R, a.E - e0);
   const int64_t next = a.ctl->next, len = a.ctl->len;
   const uint32_t step = (uint32_t)a.ctl->env_steps;
   const int64_t ep_base = a.ctl->episodes;  // advanced only by this launch's last workgroup
-  if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
+  if (a.pf_count > 0 && blockIdx.x == 0) {
     // the index draw of the step's first round, off the critical path: the
     // MT state is untouched by the env workgroups, and the length is the one
     // the last workgroup below will store (every workgroup read ctl->len
