@@ -303,7 +303,11 @@ struct mdp_handle {
   // general critic step as pairs of workgroups per 32 rows (mdp_grads_pair.hip),
   // opt-in with MDP_PAIR=1 (measured slower than k_critic_grad at S5: DESIGN §4)
   bool pair_mode = false;
-  float* pair_xa = nullptr;
+  // general critic step: the target actions by a k_target_act launch in front
+  // of k_critic_grad (MADDPG critics), opt-in with MDP_TARGET_ACT=1 (measured
+  // slower at S5: DESIGN §4); default: inside the critic kernel
+  bool target_act = false;
+  float* pair_xa = nullptr;  // [B][5 n] a~ of the pair kernel and of k_target_act
   uint32_t* pair_prod = nullptr;
   uint32_t* pair_cons = nullptr;
   hipGraph_t round_graph = nullptr;
@@ -495,6 +499,7 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.cpre_prev = post_prev;
   a.pair_xa = nullptr;
   a.pair_prod = a.pair_cons = nullptr;
+  a.xa = nullptr;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.pf_ctl = h->ctl;
@@ -539,6 +544,17 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
     a.pair_prod = h->pair_prod + (int64_t)agent * h->L.nwg;
     a.pair_cons = h->pair_cons + (int64_t)agent * h->L.nwg;
     HIPCHK(h, mdp_launch_critic_pair(a, T.H, lds_pair_bytes(T, a.group), h->stream));
+    return 0;
+  }
+  if (h->target_act && !h->L.topo.ag[agent].local_q) {  // a~ by its own launch, then the critic step
+    // one actor slot pair stays allocated: the target critic and the backward
+    // use activation slot 0 as scratch while the critic's h1 / h2 (slot G) live on
+    a.xa = h->pair_xa;
+    a.group = 1;
+    if (lds_critic_bytes(h->L.topo, 1) > MDP_LDS_BUDGET || lds_target_act_bytes(h->L.topo) > MDP_LDS_BUDGET)
+      return fail(h, "critic step does not fit in LDS");
+    HIPCHK(h, mdp_launch_target_act(a, h->L.topo.H, h->stream));
+    HIPCHK(h, mdp_launch_critic_grad(a, h->L.topo.H, lds_critic_bytes(h->L.topo, 1), h->stream));
     return 0;
   }
   // as many target actors per pass as the LDS budget allows (all of them for S1-S4)
@@ -955,6 +971,7 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
     a.cpre_prev = -1;
     a.pair_xa = nullptr;
     a.pair_prod = a.pair_cons = nullptr;
+    a.xa = nullptr;
     a.pf_ctl = h->ctl;
     a.pf_out = pf_out;
     a.pf_count = pf_out ? n * h->cfg.batch_size : 0;
@@ -1123,6 +1140,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->critic_pre = !(cp && cp[0] == '0');
     const char* pm = getenv("MDP_PAIR");
     h->pair_mode = pm && pm[0] == '1';
+    const char* ta = getenv("MDP_TARGET_ACT");
+    h->target_act = ta && ta[0] == '1';
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";

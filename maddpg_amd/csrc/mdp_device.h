@@ -959,7 +959,9 @@ __device__ __forceinline__ double sum16(double v) {
 #define MDP_NT_SLAB 0
 #endif
 __device__ __forceinline__ void slab_st(float* p, float v) {
-#if MDP_NT_SLAB
+#if MDP_NT_SLAB == 2
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through (sc1)
+#elif MDP_NT_SLAB
   __builtin_nontemporal_store(v, p);
 #else
   *p = v;

@@ -55,6 +55,10 @@ struct CriticArgs {
   float* pair_xa;
   uint32_t* pair_prod;
   uint32_t* pair_cons;
+  // general critic step (k_critic_grad): the target actions a~ [B][5 n] of
+  // every agent, computed by a k_target_act launch in front of it (k_target_act
+  // writes them here); null: the critic kernel runs the target actors itself
+  float* xa;
 };
 
 // precomputed critic-step work of one batch row (k_actor_grad_r's extra
@@ -267,6 +271,11 @@ inline int lds_actor_bytes(const Topo& t) {
   return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(S) + 5 * mdp_r4(R * 8) + mdp_r4(5 * t.H));
 }
 #define MDP_LDS_BUDGET (160 * 1024)
+// k_target_act (mdp_grads.hip): obs' rows, h1, h2, logits of 64 rows (32 at H = 256)
+inline int lds_target_act_bytes(const Topo& t) {
+  const int R = t.H == 256 ? 32 : 64, ldo = mdp_ld(t.obs_max), ldh = t.H + 1;
+  return 4 * (mdp_r4(R * ldo) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8));
+}
 // paired general critic step (mdp_grads_pair.hip): 32 rows per pair; the
 // target-actor workgroup holds obs' and G actors' h1/h2/logits, the critic
 // workgroup the rows, h1/h2 of the critic, the target critic's obs' partial,
@@ -325,6 +334,8 @@ inline int lds_eval_bytes(int in, int H) {
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
 // paired general critic step: grid 2 ceil(B / 32), a.group target actors per pass
 hipError_t mdp_launch_critic_pair(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
+// the target actions of a general critic step into a.xa: grid (ceil(B / 64), n)
+hipError_t mdp_launch_target_act(const CriticArgs& a, int H, hipStream_t s);
 hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s);

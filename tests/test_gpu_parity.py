@@ -741,3 +741,41 @@ def test_split_steps_bit_identical(monkeypatch, dims, local_q):
                 np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k} split vs unsplit")
                 np.testing.assert_array_equal(a[k], d[k], err_msg=f"{i} {w} {k} round vs per-agent")
         np.testing.assert_array_equal(on.stats(i), off.stats(i))
+
+
+@pytest.mark.parametrize("dims,local_q,B,H,general", [
+    ([22, 22, 22, 22, 20, 20], None, 1000, 128, False),  # tag N=6 (S5 shape), ragged last tile
+    ([16, 16, 16, 14], None, 512, 64, False),            # 4 target actors at H = 64
+    ([8, 10, 10], [True, False, False], 256, 64, True),  # DDPG agent keeps the in-kernel actor
+    ([22, 22, 20], None, 96, 256, False),                 # H = 256: 32-row target-action tiles
+])
+def test_target_act_launch_bit_identical(monkeypatch, dims, local_q, B, H, general):
+    """The general critic step's target actions by a k_target_act launch of
+    their own (MDP_TARGET_ACT=1) or inside k_critic_grad (default): the same
+    MFMA k-chains, heads and Gumbel noise, so three update rounds agree bit for
+    bit -- parameters, Adam slots, targets and the six stats."""
+    L = 3000
+    c = synthetic_trainer_case(dims, B, L, seed=93, local_q=local_q, H=H)
+    n = len(dims)
+    if general:
+        monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
+
+    def run():
+        eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L)
+        eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+        eng.init_params(5)
+        eng.seed_py_random(19)
+        for _ in range(3):
+            eng.update_round()
+        eng.synchronize()
+        return eng
+
+    off = run()
+    monkeypatch.setenv("MDP_TARGET_ACT", "1")
+    on = run()
+    for i in range(n):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_critic", "v_critic"):
+            a, b = on.get_params(i, w), off.get_params(i, w)
+            for k in a:
+                np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k}")
+        np.testing.assert_array_equal(on.stats(i), off.stats(i))

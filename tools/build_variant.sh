@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build the current tree's library with extra compile flags into
+# maddpg_amd/libmaddpg_hip_<name>.so (the A/B partner of tools/ab_lib.sh):
+#   bash tools/build_variant.sh wt -DMDP_NT_SLAB=2
+# Run here, not on the GPU box.
+set -e
+NAME=$1; shift
+D=/tmp/mdp_variant_$NAME
+rm -rf $D; mkdir -p $D
+mkdir -p $D/maddpg_amd $D/include; cp -r maddpg_amd/csrc $D/maddpg_amd/csrc; cp include/*.h $D/include/
+rm -rf $D/maddpg_amd/csrc/build
+make -s -C $D/maddpg_amd/csrc -j8 CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wall -Wno-unused-function $*" OUT=$D/lib.so HDR= > /dev/null
+cp $D/lib.so maddpg_amd/libmaddpg_hip_$NAME.so
+rm -rf $D
+echo "built variant $NAME ($*) -> maddpg_amd/libmaddpg_hip_$NAME.so"
