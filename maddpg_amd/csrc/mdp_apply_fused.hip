@@ -187,6 +187,10 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     const float b1p = a.beta[0], b2p = a.beta[1];  // this step's powers (advanced at the end)
     const uint32_t ep = f.phase == 3 ? f.xstep[0] + 1u : 0u;  // exchange epoch (advanced at the end)
     const uint32_t nep = f.sync_ctr[7 * 32] + 1u;                // norm-handshake epoch (advanced at the end)
+    // a fault recorded by an earlier launch, read with the first loads (not
+    // after the handshake, where its round trip would sit in front of Adam)
+    bool faulted = false;
+    if (grp == 0) faulted = __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     if (grp == 0 && act) {
       m4 = ld4(a.m + i0);
       v4 = ld4(a.v + i0);
@@ -263,6 +267,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
             __builtin_amdgcn_s_sleep(1);
             if (++it > kSpinLimit) {
               __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              faulted = true;
               break;
             }
             hi = ld_agent64(part + 2 * q);
@@ -272,9 +277,12 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
         }
         tot = wave_sum_d(tot);
       }
-      // a timed-out handshake or exchange (this launch or an earlier one)
-      // leaves the optimizer state as it was
-      const bool faulted = __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      // a timed-out handshake of this chunk, exchange of this launch or an
+      // earlier launch's fault leaves the optimizer state as it was (a chunk
+      // that saw every word of its tensor has the right norm and steps)
+      faulted = __ballot(faulted) != 0ull;
+      if (f.phase == 3)
+        faulted = faulted || __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
       if (act && !faulted) {
         const float norm = (float)sqrt(tot);
         const float clip = a.clip;
