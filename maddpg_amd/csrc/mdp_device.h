@@ -49,6 +49,13 @@ __device__ unsigned long long g_mdp_stamps[64];
   } while (0)
 #endif
 
+// A kernel's first branches each read a kernarg field, and the compiler issues
+// each read behind the previous branch: a chain of scalar-cache misses (ISA:
+// five s_load / s_waitcnt pairs before the first global load).  Naming one
+// field per 64-B line of the argument block here makes them one round trip;
+// the later reads hit the scalar cache.
+#define MDP_KARG_TOUCH(...) asm volatile("" ::__VA_ARGS__)
+
 // ------------------------------------------------------------------ RNG
 struct Philox {
   __device__ static inline uint4 round(uint4 c, uint2 k) {

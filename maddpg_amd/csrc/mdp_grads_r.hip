@@ -365,6 +365,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
 }  // namespace
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
+  MDP_KARG_TOUCH("s"(a.agent), "s"(a.inv_b), "s"(a.pf_count), "s"(a.cpre_prev), "s"(a.topo.n), "s"(gridDim.x));
   if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
     // the next round's index draw (same ring length, the MT stream continues):
     // one workgroup beside the B/16 of this kernel, so it costs no time of its own
@@ -767,6 +768,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
 }
 
 __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
+  MDP_KARG_TOUCH("s"(a.agent), "s"(a.slab_stride), "s"(a.cpre_agent), "s"(a.topo.n), "s"(gridDim.x));
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;
   __shared__ int fwd_issued;  // waves 0..3 issued the loads the critic forward needs first

@@ -5,8 +5,10 @@
 
 #include "mdp_topo.h"
 
+// Argument blocks: the scalars and pointers a kernel reads first come first and
+// the (1.7 KB) Topo last, so a kernel's opening kernarg reads share a few 64-B
+// scalar-cache lines (its early branches otherwise chained one miss each).
 struct CriticArgs {
-  Topo topo;
   int agent, B;
   const float* theta;
   const float* target;
@@ -59,6 +61,7 @@ struct CriticArgs {
   // every agent, computed by a k_target_act launch in front of it (k_target_act
   // writes them here); null: the critic kernel runs the target actors itself
   float* xa;
+  Topo topo;
 };
 
 // precomputed critic-step work of one batch row (k_actor_grad_r's extra
@@ -75,7 +78,6 @@ struct CriticArgs {
 #define MDP_APRE_W 144
 
 struct ActorArgs {
-  Topo topo;
   int agent, B;
   const float* theta;
   const float* replay;
@@ -99,6 +101,7 @@ struct ActorArgs {
   int cpre_agent;
   const int32_t* cpre_idx;
   const float* target;        // target nets (the critic_pre role's target actors / critic)
+  Topo topo;
 };
 
 struct ReduceArgs {
@@ -115,7 +118,6 @@ struct ReduceArgs {
 #define MDP_APPLY_CHUNK 1024  // parameters per apply workgroup
 
 struct ApplyArgs {
-  NDesc net, other;
   int blk[7], oblk[7];  // prefix counts of chunk workgroups per tensor (net / other)
   float* theta;
   float* target;
@@ -137,6 +139,7 @@ struct ApplyArgs {
   uint32_t* ticket;
   Ctl* ctl;
   int bump_ctr;         // the last workgroup advances Ctl::upd_ctr by this much
+  NDesc net, other;
 };
 
 // k_reduce_apply (mdp_apply_fused.hip): batch reduction + optimizer step in one launch
@@ -167,22 +170,22 @@ inline int64_t mdp_xch_bytes(int world, int64_t param_floats) {
 }
 
 struct FusedApplyArgs {
-  ApplyArgs ap;         // ap.slab / nwg / slab_stride: the partial gradients
+  int pf_count;         // (below)
+  int phase;            // 0 reduce + step; 1 reduce into grad[] only; 2 step from grad[] (all-reduced);
+                        // 3 reduce, xGMI exchange with every rank (xd), step x ap.scale
   int rblk[7];          // prefix counts of MDP_RA_CHUNK workgroups per tensor of ap.net
   uint32_t* sync_ctr;   // 6 tensor counters of this (agent, net), 32 words apart
   uint64_t* sync_part;  // [6][MDP_RA_MAXCH][2] published sums of squares (epoch-tagged halves)
   uint32_t* done_ctr;   // workgroups finished (last one advances beta)
-  int phase;            // 0 reduce + step; 1 reduce into grad[] only; 2 step from grad[] (all-reduced);
-                        // 3 reduce, xGMI exchange with every rank (xd), step x ap.scale
   const XchgDesc* xd;   // phase 3: device copy of the exchange descriptor
   int net_id;           // phase 3: 2 * agent + net (epoch counter)
   uint32_t* xstep;      // phase 3: Ctl::xstep[net_id], exchanges done for this net
-  // > 0: one extra (last) workgroup draws pf_count indices of the NEXT round
-  // into pf_out, continuing the MT19937 stream (a piece of the draw the fast
-  // kernels make beside the critic step; general-kernel configurations)
-  int pf_count;
+  // pf_count > 0: one extra (last) workgroup draws pf_count indices of the NEXT
+  // round into pf_out, continuing the MT19937 stream (a piece of the draw the
+  // fast kernels make beside the critic step; general-kernel configurations)
   int32_t* pf_out;
   Ctl* pf_ctl;
+  ApplyArgs ap;         // ap.slab / nwg / slab_stride: the partial gradients
 };
 // sync area: per (agent, net) 8 counters x 128 B (6 done, 7 norm epoch), then [6][MAXCH][2] tagged words
 inline int64_t mdp_ra_sync_bytes() {
