@@ -428,7 +428,8 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
 
 __global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
   MDP_KARG_TOUCH("s"(f.pf_count), "s"(f.xstep), "s"(f.ap.blk[0]), "s"(f.ap.target), "s"(f.ap.clip), "s"(f.ap.stats_mode),
-                 "s"(f.ap.ctl), "s"(f.ap.net.t[0].off), "s"(gridDim.x));
+                 "s"(f.ap.ctl), "s"(gridDim.x), "s"(f.ap.net.t[0].off), "s"(f.ap.net.t[4].cols), "s"(f.ap.other.t[2].off),
+                 "s"(f.ap.other.in));
   if (f.pf_count > 0 && blockIdx.x == gridDim.x - 1) {  // a piece of the next round's index draw
     make_index_block<1024>(f.pf_ctl, f.pf_count, f.pf_out);
     return;

@@ -55,6 +55,10 @@ __device__ unsigned long long g_mdp_stamps[64];
 // field per 64-B line of the argument block here makes them one round trip;
 // the later reads hit the scalar cache.
 #define MDP_KARG_TOUCH(...) asm volatile("" ::__VA_ARGS__)
+// every 64-B line of two agents' descriptors (212 B each: fields at most 56 B
+// apart), once the kernel knows which agents it serves -- one round trip
+#define MDP_KARG_ADESC(d) "s"((d).actor.t[0].off), "s"((d).actor.t[3].rows), "s"((d).actor.in), \
+                          "s"((d).critic.t[2].off), "s"((d).critic.in), "s"((d).cin)
 
 // ------------------------------------------------------------------ RNG
 struct Philox {

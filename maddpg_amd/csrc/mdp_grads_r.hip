@@ -391,6 +391,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   const int32_t* idx = a.multi > 1 ? a.idx + (int64_t)agent * a.B : a.idx;
   const float* u_tgt = (a.multi > 1 && a.u_tgt) ? a.u_tgt + (int64_t)agent * a.topo.n * a.B * MDP_ACT_DIM : a.u_tgt;
   const Topo& T = a.topo;
+  MDP_KARG_TOUCH(MDP_KARG_ADESC(T.ag[agent]), MDP_KARG_ADESC(T.ag[max(a.cpre_prev, 0)]));
   const ADesc& ag = T.ag[agent];
   const NDesc& nd = ag.critic;
   const bool lq = ag.local_q != 0;
@@ -788,6 +789,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   const int32_t* idx = a.multi > 1 ? a.idx + (int64_t)agent * a.B : a.idx;
   const float* u_act = (a.multi > 1 && a.u_act) ? a.u_act + (int64_t)agent * a.B * MDP_ACT_DIM : a.u_act;
   const Topo& T = a.topo;
+  MDP_KARG_TOUCH(MDP_KARG_ADESC(T.ag[agent]));
   const ADesc& ag = T.ag[agent];
   const NDesc& na = ag.actor;
   const NDesc& nc = ag.critic;
