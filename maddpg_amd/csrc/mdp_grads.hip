@@ -463,6 +463,8 @@ static_assert(MDP_GEN_THREADS / 64 >= MDP_MAX_UNITS / 16, "one single-net layer 
 
 template <int H>
 __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
+  // (no MDP_KARG_TOUCH here: at H = 128 it turned the kernel's 47 spilled
+  // SGPRs into 91 spilled VGPRs)
   constexpr int NT = H / 16;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Topo& T = a.topo;
@@ -763,6 +765,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
 
 template <int H>
 __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
+  MDP_KARG_TOUCH("s"(a.agent), "s"(a.slab_stride), "s"(a.cpre_agent), "s"(a.topo.n));
+  MDP_KARG_TOUCH(MDP_KARG_ADESC(a.topo.ag[a.agent]));
   constexpr int NT = H / 16;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Topo& T = a.topo;
