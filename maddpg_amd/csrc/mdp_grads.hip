@@ -496,6 +496,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   float* qv = lg + G * MDP_R * 8;
   float pf[MDP_KC];  // this wave's next single-net layer chunk, issued ahead (wave < NT)
   f32x4 pft[4];      // the backward's first W^T chunk, issued ahead
+  constexpr int HKS = H / 4 <= 32 ? H / 4 : 1;  // head fragments per lane (the target critic's, issued ahead)
   MDP_STAMP(0);
 
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
@@ -679,6 +680,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
 
   // target critic Q'(o', a~) over all waves; wave 0: head, fp64 TD target
   // (maddpg.py:186), loss partials, dL/dq = 2(q-y)/B
+  float thw[HKS], thb = 0.f;  // the target critic's head fragments, issued with its layer 2 (wave 0)
   {
     const float* P = a.target;
     if (wave < NT) {  // (a prefetch of this layer across the layer phases would spill)
@@ -689,6 +691,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     }
     __syncthreads();
     if (wave < NT) {
+      if (H / 4 <= 32 && wave == 0) head_load<HKS>(thw, thb, P + nd.t[4].off, P + nd.t[5].off, 1);
       fwd_tile_pf<true>(hA, ldh, 0, H, P + nd.t[2].off, P + nd.t[3].off, H, nullptr, 0, hB, ldh, wave, pf);
       pf_load_t(pft, a.theta + nd.t[2].off, H, wave);  // the backward's dh1 = d2 W2^T
     }
@@ -696,7 +699,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   }
   if (wave == 0) {
     const float* P = a.target;
-    head_mfma<H / 4>(hB, ldh, H, P + nd.t[4].off, P + nd.t[5].off, 1, lg, 8);
+    if constexpr (H / 4 <= 32) head_acc<HKS>(thw, thb, hB, ldh, 1, lg, 8);
+    else head_mfma<H / 4>(hB, ldh, H, P + nd.t[4].off, P + nd.t[5].off, 1, lg, 8);
     wave_sync();
     double s_l = 0.0, s_y = 0.0, s_r = 0.0, s_q = 0.0;
     float g = 0.f;
