@@ -37,6 +37,29 @@
 #include "mdp_kernels.h"
 #include "mdp_mt.h"
 
+// diagnostic build: every workgroup's start (wave 0) and per-wave end of the
+// last critic (k = 0) / actor (k = 1) launch -- which role ends the launch
+#ifdef MDP_STAMPS
+__device__ unsigned long long g_wg_t0[2][512];
+__device__ unsigned long long g_wg_t1[2][512][8];
+#define MDP_WG_START(k)                                                               \
+  do {                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 512) g_wg_t0[k][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define MDP_WG_END(k)                                                                 \
+  do {                                                                                \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 512)                                  \
+      g_wg_t1[k][blockIdx.x][threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define MDP_WG_START(k) \
+  do {                  \
+  } while (0)
+#define MDP_WG_END(k) \
+  do {                \
+  } while (0)
+#endif
+
 namespace {
 constexpr int RH = MDP_RH, LH = MDP_RLH, LD = MDP_RLD;
 
@@ -366,10 +389,12 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   MDP_KARG_TOUCH("s"(a.agent), "s"(a.inv_b), "s"(a.pf_count), "s"(a.cpre_prev), "s"(a.topo.n), "s"(gridDim.x));
+  MDP_WG_START(0);
   if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
     // the next round's index draw (same ring length, the MT stream continues):
     // one workgroup beside the B/16 of this kernel, so it costs no time of its own
     make_index_block<512>(a.pf_ctl, a.pf_count, a.pf_out);
+    MDP_WG_END(0);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -380,6 +405,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
     if (bx >= nwg) {
       actor_pre_tile(a, lds, &rows_ready, bx - nwg);
+      MDP_WG_END(0);
       return;
     }
   }
@@ -766,6 +792,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   if (kb_c) wgrad_waves(rowbuf + ag.act_off, ldr, kb_c, d1, LD, RH, slab + nd.t[0].off + ka_c * RH, 0, 8);
   if (wave == 7) colsum64(d1, LD, slab + nd.t[1].off);
   MDP_STAMP(10);
+  MDP_WG_END(0);
 }
 
 __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
@@ -773,11 +800,13 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;
   __shared__ int fwd_issued;  // waves 0..3 issued the loads the critic forward needs first
+  MDP_WG_START(1);
   int agent = a.agent, bx = blockIdx.x;
   if (a.cpre) {  // workgroups [B/16, 2 B/16): the next critic step's independent work (strict mode)
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
     if (bx >= nwg) {
       critic_pre_tile(a, lds, &rows_ready, bx - nwg);
+      MDP_WG_END(1);
       return;
     }
   }
@@ -1005,6 +1034,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   wgrad_waves(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1a, LD, RH, slab + na.t[0].off, 0, 8);
   if (wave == 7) colsum64(d1a, LD, slab + na.t[1].off);
   MDP_STAMP(27);
+  MDP_WG_END(1);
 }
 
 namespace {
@@ -1037,5 +1067,10 @@ hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_
 // diagnostic build: stamps of this translation unit's kernels (own code object)
 extern "C" int mdp_debug_stamps_r(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+// [2][512] starts, then [2][512][8] per-wave ends
+extern "C" int mdp_debug_wg_times(unsigned long long* t0, unsigned long long* t1) {
+  if (hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_wg_t0), sizeof(unsigned long long) * 2 * 512) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(t1, HIP_SYMBOL(g_wg_t1), sizeof(unsigned long long) * 2 * 512 * 8) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -1,0 +1,47 @@
+"""Diagnostic: which workgroup role ends each fast gradient launch (S2).
+
+    make -C maddpg_amd/csrc stamps
+    MDP_LIB=maddpg_amd/libmaddpg_hip_stamps.so python tools/wg_times.py
+Per role of the last k_critic_grad_r / k_actor_grad_r launch of a round:
+the earliest start, the latest start and the latest end, in us after the
+launch's first workgroup started (s_memrealtime, 100 MHz)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from maddpg_amd import _lib  # noqa: E402
+from maddpg_amd.engine import Engine  # noqa: E402
+
+assert "stamps" in _lib.LIB_PATH
+eng = Engine([18, 18, 18], batch_size=1024, capacity=30000)
+eng.add_rows(torch.rand(eng.capacity, eng.row_stride))
+eng.init_params(0)
+eng.seed_py_random(0)
+lib = _lib.load()
+fn = lib.mdp_debug_wg_times
+fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
+for it in range(5):
+    eng.update_round()
+    eng.synchronize()
+t0 = (ctypes.c_ulonglong * (2 * 512))()
+t1 = (ctypes.c_ulonglong * (2 * 512 * 8))()
+assert fn(t0, t1) == 0
+t0 = np.array(t0[:], dtype=np.int64).reshape(2, 512)
+t1 = np.array(t1[:], dtype=np.int64).reshape(2, 512, 8)
+nwg = 64
+for k, name, roles in ((0, "critic launch", [("critic step", 0, nwg), ("actor_pre", nwg, 2 * nwg), ("draw", 2 * nwg, 2 * nwg + 1)]),
+                       (1, "actor launch", [("actor step", 0, nwg), ("critic_pre", nwg, 2 * nwg)])):
+    used = t0[k] > 0
+    base = t0[k][used].min()
+    print(name)
+    for rn, lo, hi in roles:
+        s = t0[k][lo:hi]
+        if not (s > 0).any():
+            continue
+        e = t1[k][lo:hi].max(axis=1)
+        print(f"  {rn:>12s}: start {(s.min() - base) / 100:5.2f}..{(s.max() - base) / 100:5.2f} us, "
+              f"end median {(np.median(e) - base) / 100:5.2f}, max {(e.max() - base) / 100:5.2f} us")
