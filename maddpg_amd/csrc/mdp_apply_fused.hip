@@ -231,6 +231,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       f32x4 g = red[0][col];
 #pragma unroll
       for (int q = 1; q < 16; ++q) g += red[q][col];
+      MDP_STAMP(34);
       if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ep);
       double ss = 0.0;
 #pragma unroll
@@ -239,11 +240,17 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
         if (p0 + j < n) ss += (double)gs * (double)gs;
       }
       ss = wave_sum_d(ss);
+      MDP_STAMP(35);
       if (act && f.phase != 2) {
+        if (p0 + 3 < n) {
+          *reinterpret_cast<f32x4*>(a.grad + i0) = g;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (p0 + j < n) a.grad[i0 + j] = g[j];
+          for (int j = 0; j < 4; ++j)
+            if (p0 + j < n) a.grad[i0 + j] = g[j];
+        }
       }
+      MDP_STAMP(36);
       double tot = ss;
       if (f.phase != 1) {  // phase 1 (data parallel) stops here: the all-reduce follows
       if (nch > 1) {
@@ -283,6 +290,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       faulted = __ballot(faulted) != 0ull;
       if (f.phase == 3)
         faulted = faulted || __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      MDP_STAMP(37);
       if (act && !faulted) {
         const float norm = (float)sqrt(tot);
         const float clip = a.clip;
@@ -290,17 +298,29 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
         const float one = 1.0f;
         const float alpha = a.lr * sqrtf(one - b2p) / (one - b1p);
         const float c1 = one - a.b1, c2 = one - a.b2;
+        f32x4 mo, vo, tho, tgo;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (p0 + j < n) {
-            const float gc = ((g[j] * a.scale) * clip) / denom;
-            const float m = m4[j] + (gc - m4[j]) * c1;
-            const float v = v4[j] + (gc * gc - v4[j]) * c2;
-            const float th = th4[j] - (m * alpha) / (sqrtf(v) + a.eps);
-            a.m[i0 + j] = m;
-            a.v[i0 + j] = v;
-            a.theta[i0 + j] = th;
-            if (a.polyak) a.target[i0 + j] = a.pa * tg4[j] + a.pb * th;
+          const float gc = ((g[j] * a.scale) * clip) / denom;
+          mo[j] = m4[j] + (gc - m4[j]) * c1;
+          vo[j] = v4[j] + (gc * gc - v4[j]) * c2;
+          tho[j] = th4[j] - (mo[j] * alpha) / (sqrtf(vo[j]) + a.eps);
+          tgo[j] = a.pa * tg4[j] + a.pb * tho[j];
+        }
+        if (p0 + 3 < n) {  // the whole float4 in the tensor: one 16-B store per array
+          *reinterpret_cast<f32x4*>(a.m + i0) = mo;
+          *reinterpret_cast<f32x4*>(a.v + i0) = vo;
+          *reinterpret_cast<f32x4*>(a.theta + i0) = tho;
+          if (a.polyak) *reinterpret_cast<f32x4*>(a.target + i0) = tgo;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (p0 + j < n) {
+              a.m[i0 + j] = mo[j];
+              a.v[i0 + j] = vo[j];
+              a.theta[i0 + j] = tho[j];
+              if (a.polyak) a.target[i0 + j] = tgo[j];
+            }
           }
         }
       }

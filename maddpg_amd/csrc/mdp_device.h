@@ -98,10 +98,28 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// fp64 wave sum on DPP moves (each a VALU op on the lane crossbar) instead of
+// six ds_bpermute round trips through the LDS crossbar (stamped 0.4 us of the
+// optimizer's critical path): xor 1, xor 2, half-row mirror, row mirror (every
+// lane holds its row's sum), row_bcast15 / row_bcast31 fold the rows into lane
+// 63, read back to every lane.  A fixed tree: deterministic.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_d<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_d<0x140, 0xf>(v);  // row_mirror
+  v += dpp_d<0x142, 0xa>(v);  // row_bcast15 into rows 1, 3
+  v += dpp_d<0x143, 0xc>(v);  // row_bcast31 into rows 2, 3
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
 // workgroup-wide sum (all threads get the result); scratch >= MDP_NW doubles

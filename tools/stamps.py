@@ -102,3 +102,8 @@ if lib_ra is not None:
         print("k_reduce_apply wg 0 (last launch): partial loads + combine %.2f us, norm handshake %.2f us, "
               "clip/Adam/stores %.2f us" % ((ra[31] - ra[30]) * 10 / 1000, (ra[32] - ra[31]) * 10 / 1000,
                                             (ra[33] - ra[32]) * 10 / 1000))
+    if ra[34]:
+        us = lambda a_, b_: (ra[b_] - ra[a_]) * 10 / 1000
+        print("  detail: barrier -> 16-group combine %.2f, sum of squares %.2f, grad stores %.2f, publish %.2f, "
+              "poll %.2f, Adam + stores %.2f us" % (us(31, 34), us(34, 35), us(35, 36), us(36, 32), us(32, 37),
+                                                    us(37, 33)))
