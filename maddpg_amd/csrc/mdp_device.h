@@ -98,6 +98,32 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Sums over lane groups on DPP moves (VALU ops on the lane crossbar) instead of
+// __shfl_xor, which lowers to ds_bpermute round trips through the LDS
+// crossbar.  quad_perm [1,0,3,2] / [2,3,0,1] are exactly xor 1 / xor 2; once
+// every quad holds its sum, the half-row and row mirrors pair the same partial
+// sums as xor 4 / xor 8, so quad_sum / row_sum are bit-identical to those
+// butterflies.  Every lane of the wave must be active.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float quad_sum(float s) {  // = s + shfl_xor 1, then + shfl_xor 2
+  s += dpp_f<0xB1>(s);
+  s += dpp_f<0x4E>(s);
+  return s;
+}
+__device__ __forceinline__ float half_row_sum(float s) {  // ... then + shfl_xor 4
+  s = quad_sum(s);
+  s += dpp_f<0x141>(s);
+  return s;
+}
+__device__ __forceinline__ float row_sum(float s) {  // ... then + shfl_xor 8
+  s = half_row_sum(s);
+  s += dpp_f<0x140>(s);
+  return s;
+}
+
 // fp64 wave sum on DPP moves (each a VALU op on the lane crossbar) instead of
 // six ds_bpermute round trips through the LDS crossbar (stamped 0.4 us of the
 // optimizer's critical path): xor 1, xor 2, half-row mirror, row mirror (every
@@ -366,8 +392,7 @@ __device__ __forceinline__ void tile_head(const float* X, int ldx, int K, const 
       const int row = o / nout, c = o - row * nout;
       for (int k = q; k < K; k += 4) s = fmaf(X[row * ldx + k], W[k * nout + c], s);
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
+    s = quad_sum(s);
     if (o < total && q == 0) {
       const int row = o / nout, c = o - row * nout;
       out[row * ldo + c] = s + b[c];
@@ -544,8 +569,7 @@ __device__ __forceinline__ void head_phase(const HJob* jobs, int njobs, int K, f
     const float* W = (h.wsel ? P1 : P0) + h.woff;
     if (ok)
       for (int k = q; k < K; k += 4) s = fmaf(X[row * h.ldx + k], W[k * h.nout + c], s);
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
+    s = quad_sum(s);
     if (ok && q == 0) lds[h.ooff + row * h.ldo + c] = s + (h.wsel ? P1 : P0)[h.boff + c];
   }
 }
@@ -607,8 +631,7 @@ __device__ __forceinline__ void wave_head(const float* X, int ldx, int K, const 
     const int row = ok ? o / nout : 0, c = ok ? o - row * nout : 0;
     float s = 0.f;
     for (int k = q; k < K; k += 4) s = fmaf(X[row * ldx + k], W[k * nout + c], s);
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
+    s = quad_sum(s);
     if (ok && q == 0) out[row * ldo + c] = s + b[c];
   }
   wave_sync();
@@ -892,9 +915,7 @@ __device__ __forceinline__ float rq_head(const float* X, int ldx, const float (&
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) s = fmaf(X[row * ldx + 4 * j + q], w[j], s);
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  return s;
+  return quad_sum(s);
 }
 
 // one 16-column tile per wave (column col = 16 tt + r of W[K][ldw]), k = 4s + kq;
@@ -972,11 +993,13 @@ __device__ __forceinline__ void lds_wait(int* flag, int n) {
 
 // ------------------------------------------------ shared by the grad kernels
 // lanes 0..15 hold one value each; returns the sum in every lane (fixed order)
-__device__ __forceinline__ double sum16(double v) {
+__device__ __forceinline__ double sum16(double v) {  // lanes 0..15 (every lane of row 0 gets it)
   const int lane = threadIdx.x & 63;
   v = lane < MDP_R ? v : 0.0;
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += dpp_d<0xB1, 0xf>(v);
+  v += dpp_d<0x4E, 0xf>(v);
+  v += dpp_d<0x141, 0xf>(v);
+  v += dpp_d<0x140, 0xf>(v);
   return v;
 }
 

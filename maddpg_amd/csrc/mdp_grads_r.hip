@@ -98,10 +98,7 @@ __device__ __forceinline__ void critic_l2_tile(const float* h1, const float (&w2
     const float h = fmaxf(acc[i] + b2t, 0.f);
     d2[row * LD + col] = (row < nvalid && h > 0.f) ? dq * w3t : 0.f;
     float s = h * w3t;  // sum over the 16 columns (lanes r of this kq group), fixed order
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    s += __shfl_xor(s, 8, 64);
+    s = row_sum(s);
     if (r == 0) qpart[tt * MDP_R + row] = s;
   }
 }

@@ -206,9 +206,7 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs a) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += v[k];
   }
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
+  s = half_row_sum(s);
   if (el < a.size && q == 0) a.grad[a.off + el] = s;
 }
 
