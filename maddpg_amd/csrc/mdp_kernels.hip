@@ -549,20 +549,24 @@ __device__ inline void env_bench(const EnvDesc& E, const float* p, int goal, flo
 
 // World.step (core.py): action force, pairwise soft contact, damping,
 // integration with max_speed clamp.  p, v: [ne][2] of one env (in place).
-__device__ inline void env_physics(const EnvDesc& E, float* p, float* v, const float* act /*[n][5]*/) {
+// f: this env's force scratch [3][MDP_MAX_ENT] in LDS (fx, fy, has) -- as
+// private arrays with runtime indices they lived in scratch memory, a
+// read-modify-write round trip through the vector memory path per contact
+__device__ inline void env_physics(const EnvDesc& E, float* p, float* v, const float* act /*[n][5]*/, float* f) {
   const int n = E.n_agents, ne = E.n_agents + E.n_landmarks;
-  float fx[MDP_MAX_ENT], fy[MDP_MAX_ENT];
-  bool has[MDP_MAX_ENT];
+  float* fx = f;
+  float* fy = f + MDP_MAX_ENT;
+  float* has = f + 2 * MDP_MAX_ENT;
   for (int e = 0; e < ne; ++e) {
     fx[e] = 0.f;
     fy[e] = 0.f;
-    has[e] = false;
+    has[e] = 0.f;
   }
   for (int i = 0; i < n; ++i) {  // environment._set_action, discrete action space
     const float* a = act + i * MDP_ACT_DIM;
     fx[i] = (a[1] - a[2]) * E.accel[i];
     fy[i] = (a[3] - a[4]) * E.accel[i];
-    has[i] = true;
+    has[i] = 1.f;
   }
   const float k = 1e-3f;  // contact_margin
   for (int a = 0; a < ne; ++a) {
@@ -577,19 +581,19 @@ __device__ inline void env_physics(const EnvDesc& E, float* p, float* v, const f
       if (E.movable[a]) {
         fx[a] = sx + fx[a];
         fy[a] = sy + fy[a];
-        has[a] = true;
+        has[a] = 1.f;
       }
       if (E.movable[b]) {
         fx[b] = -sx + fx[b];
         fy[b] = -sy + fy[b];
-        has[b] = true;
+        has[b] = 1.f;
       }
     }
   }
   for (int e = 0; e < ne; ++e) {
     if (!E.movable[e]) continue;
     float vx = v[2 * e] * (1.f - 0.25f), vy = v[2 * e + 1] * (1.f - 0.25f);
-    if (has[e]) {
+    if (has[e] != 0.f) {
       vx += (fx[e] / 1.f) * 0.1f;
       vy += (fy[e] / 1.f) * 0.1f;
     }
@@ -700,6 +704,7 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   float* lg = cv.take(MDP_R * 8);
   float* sp = cv.take(MDP_R * 2 * MDP_MAX_ENT);
   float* sv = cv.take(MDP_R * 2 * MDP_MAX_ENT);
+  float* sfo = cv.take(MDP_R * 3 * MDP_MAX_ENT);  // per-env force scratch of env_physics
 
   const int tid = threadIdx.x;
   // with a draw workgroup it is block 0 (dispatched first: at tag6 B=4096 the
@@ -767,11 +772,11 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     float* p = sp + tid * 2 * MDP_MAX_ENT;
     float* v = sv + tid * 2 * MDP_MAX_ENT;
     float* row = rowt + tid * ldr;
-    float actv[MDP_MAX_AGENTS * MDP_ACT_DIM];
-    for (int j = 0; j < n; ++j)
-      for (int k = 0; k < MDP_ACT_DIM; ++k) actv[j * MDP_ACT_DIM + k] = row[T.ag[j].act_off + k];
-    env_physics(E, p, v, actv);
-    float rew[MDP_MAX_AGENTS];
+    // the row's actions act_0 .. act_{n-1} and rewards rew_0 .. rew_{n-1} are
+    // contiguous (mdp_topo.h): read and written in place, not through private
+    // arrays (scratch memory)
+    env_physics(E, p, v, row + T.ag[0].act_off, sfo + tid * 3 * MDP_MAX_ENT);
+    float* rew = row + T.ag[0].rew_off;
     env_reward(E, p, goal, rew);
     if (a.bench) env_bench(E, p, goal, a.bench + (int64_t)(e0 + tid) * n * MDP_BENCH_W);
     for (int j = 0; j < n; ++j) {
