@@ -60,6 +60,20 @@ __device__ unsigned long long g_mdp_stamps[64];
 #define MDP_KARG_ADESC(d) "s"((d).actor.t[0].off), "s"((d).actor.t[3].rows), "s"((d).actor.in), \
                           "s"((d).critic.t[2].off), "s"((d).critic.in), "s"((d).cin)
 
+// The training-noise counter (Ctl::upd_ctr, advanced by the previous
+// optimizer launch) is a uniform load from memory another kernel wrote: the
+// compiler turned it into an SGPR with v_readfirstlane right after the load and
+// waited for it there -- every wave stalled a memory round trip (ISA:
+// global_load + s_waitcnt vmcnt(0) in front of B0) before issuing its weight
+// loads.  ctr_load issues the load where it stands; ctr_use makes the VGPR
+// opaque where the noise is made, so the wait moves there (behind the weight
+// loads, which are still in flight).
+__device__ __forceinline__ uint32_t ctr_load(const Ctl* ctl) { return ctl->upd_ctr; }
+__device__ __forceinline__ uint32_t ctr_use(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // ------------------------------------------------------------------ RNG
 struct Philox {
   __device__ static inline uint4 round(uint4 c, uint2 k) {

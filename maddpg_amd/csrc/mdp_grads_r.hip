@@ -161,7 +161,7 @@ __device__ __forceinline__ void actor_fwd_wave(const float* __restrict__ P, cons
     if (u_act) {
       for (int k = 0; k < MDP_ACT_DIM; ++k) u[k] = lane < nvalid ? u_act[(int64_t)(r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
     } else {
-      uniforms5(seed, (uint32_t)((agent << 8) | 0x80), ctr, (uint32_t)(r0 + (lane & 15)), u);
+      uniforms5(seed, (uint32_t)((agent << 8) | 0x80), ctr_use(ctr), (uint32_t)(r0 + (lane & 15)), u);
     }
     gumbel_noise5(u, gn);
   }
@@ -216,7 +216,7 @@ __device__ __forceinline__ void actor_pre_tile(const CriticArgs& a, float* lds, 
   if (threadIdx.x == 0) *rows_ready = 0;
   __syncthreads();
   if (wave == 0) {
-    actor_fwd_wave(a.theta, ag.actor, ag, rowbuf, ldr, a.u_act, nvalid, r0, a.seed, a.agent, a.ctl->upd_ctr,
+    actor_fwd_wave(a.theta, ag.actor, ag, rowbuf, ldr, a.u_act, nvalid, r0, a.seed, a.agent, ctr_load(a.ctl),
                    rows_ready, 7, h1a, h2a, lg, av);
   } else {
     gather_rows16_part(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr, 64, 448);
@@ -269,7 +269,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int r0 = bx * MDP_R, nvalid = min(MDP_R, a.B - r0);
-  const uint32_t ctr = a.ctl->upd_ctr + 1u;  // critic k runs after p's actor step advanced the counter
+  const uint32_t ctr = ctr_load(a.ctl) + 1u;  // critic k runs after p's actor step advanced the counter
   const float* Pc = a.theta;
   const float* Pt = a.target;
   if (threadIdx.x == 0) *rows_ready = 0;
@@ -289,7 +289,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
       float gn[MDP_ACT_DIM];
       {
         float u[MDP_ACT_DIM];
-        uniforms5(a.seed, (uint32_t)((k << 8) | (j + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
+        uniforms5(a.seed, (uint32_t)((k << 8) | (j + 1)), ctr_use(ctr), (uint32_t)(r0 + (lane & 15)), u);
         gumbel_noise5(u, gn);
       }
       lds_wait(rows_ready, 4);
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int r0 = bx * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
-  const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)agent : 0u);
+  const uint32_t ctr = ctr_load(a.ctl) + (a.multi > 1 ? (uint32_t)agent : 0u);
   const float* Pc = a.theta;
   const float* Pt = a.target;
   // critic_post: target actor pprev is the only one left (see CriticArgs::cpre)
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         rh_load(w3, Pt + an.t[4].off, MDP_ACT_DIM);
         b3 = Pt[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
         float u[MDP_ACT_DIM];
-        uniforms5(a.seed, (uint32_t)((agent << 8) | (pprev + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
+        uniforms5(a.seed, (uint32_t)((agent << 8) | (pprev + 1)), ctr_use(ctr), (uint32_t)(r0 + (lane & 15)), u);
         gumbel_noise5(u, gn);
       }
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
           for (int k = 0; k < MDP_ACT_DIM; ++k)
             u[k] = lane < nvalid ? u_tgt[((int64_t)j * a.B + r0 + lane) * MDP_ACT_DIM + k] : 0.5f;
         } else {
-          uniforms5(a.seed, (uint32_t)((agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + (lane & 15)), u);
+          uniforms5(a.seed, (uint32_t)((agent << 8) | (j + 1)), ctr_use(ctr), (uint32_t)(r0 + (lane & 15)), u);
         }
         gumbel_noise5(u, gn);
       }
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int r0 = bx * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
-  const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)agent : 0u);
+  const uint32_t ctr = ctr_load(a.ctl) + (a.multi > 1 ? (uint32_t)agent : 0u);
   const float* P = a.theta;
   // critic L1 replay-part contraction split over waves 1..3 (KC rows each)
   constexpr int KC = 28, KSC = KC / 4;
