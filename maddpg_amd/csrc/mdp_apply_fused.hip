@@ -189,8 +189,11 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     const uint32_t nep = f.sync_ctr[7 * 32] + 1u;                // norm-handshake epoch (advanced at the end)
     // a fault recorded by an earlier launch, read with the first loads (not
     // after the handshake, where its round trip would sit in front of Adam)
+    // (kept an opaque VGPR until the step: compared here, the compiler waited
+    // for the load in front of the partial loads)
+    uint32_t fault0 = 0u;
+    if (grp == 0) fault0 = __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool faulted = false;
-    if (grp == 0) faulted = __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     if (grp == 0 && act) {
       m4 = ld4(a.m + i0);
       v4 = ld4(a.v + i0);
@@ -287,7 +290,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       // a timed-out handshake of this chunk, exchange of this launch or an
       // earlier launch's fault leaves the optimizer state as it was (a chunk
       // that saw every word of its tensor has the right norm and steps)
-      faulted = __ballot(faulted) != 0ull;
+      faulted = __ballot(faulted || ctr_use(fault0) != 0u) != 0ull;
       if (f.phase == 3)
         faulted = faulted || __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
       MDP_STAMP(37);
