@@ -705,16 +705,24 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   float* sp = cv.take(MDP_R * 2 * MDP_MAX_ENT);
   float* sv = cv.take(MDP_R * 2 * MDP_MAX_ENT);
   float* sfo = cv.take(MDP_R * 3 * MDP_MAX_ENT);  // per-env force scratch of env_physics
+  float* epr = cv.take(MDP_R * MDP_MAX_AGENTS);    // the envs' running episode rewards
 
   const int tid = threadIdx.x;
   // with a draw workgroup it is block 0 (dispatched first: at tag6 B=4096 the
   // draw is 24,576 indices) and the env copies start at block 1
   const int e0 = ((int)blockIdx.x - (a.pf_count > 0 ? 1 : 0)) * MDP_R;
   const int nvalid = min(MDP_R, a.E - e0);
-  const int64_t next = a.ctl->next, len = a.ctl->len;
-  const uint32_t step = (uint32_t)a.ctl->env_steps;
-  const int64_t ep_base = a.ctl->episodes;  // advanced only by this launch's last workgroup
+  // Ctl fields written by earlier launches: issued here, consumed as opaque
+  // VGPRs where they are used (ctr_use) -- made SGPRs at the load, they were
+  // waited for in front of the state loads
+  // (through a VGPR copy of the pointer: as scalar loads they shared lgkmcnt
+  // with the kernarg reads, and the first kernarg wait waited for them too)
+  const Ctl* ctlv = a.ctl;
+  asm volatile("" : "+v"(ctlv));
+  typedef __attribute__((address_space(1))) const Ctl gCtl;  // global, not FLAT
+  const gCtl* gc = (const gCtl*)ctlv;
   if (a.pf_count > 0 && blockIdx.x == 0) {
+    const int64_t next = gc->next, len = gc->len;
     // the index draw of the step's first round, off the critical path: the
     // MT state is untouched by the env workgroups, and the length is the one
     // the last workgroup below will store (every workgroup read ctl->len
@@ -724,26 +732,53 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     return;
   }
 
-  for (int q = tid; q < MDP_R * 2 * ne; q += MDP_NT) {
-    const int r = q / (2 * ne), c = q - r * 2 * ne;
-    float pv = 0.f, vv = 0.f;
-    if (r < nvalid) {
-      pv = a.pos[(int64_t)(e0 + r) * 2 * ne + c];
-      vv = a.vel[(int64_t)(e0 + r) * 2 * ne + c];
+  MDP_STAMP(40);
+  // every env-state load of the step issued up front (the episode bookkeeping
+  // read ep_rew / ep_step from memory in the physics phase: a round trip there)
+  // (all loads first, then the LDS stores: a load-store loop waited for each
+  // load before the next loop's loads issued; goal / ep_step stay opaque
+  // VGPRs until used, or the compiler waits for them right here)
+  int goal = 0, ep_st = 0;
+  if (tid < MDP_R && tid < nvalid) {
+    goal = a.goal[e0 + tid];
+    ep_st = a.ep_step[e0 + tid];
+  }
+  static_assert(MDP_R * 2 * MDP_MAX_ENT <= 2 * MDP_NT && MDP_R * MDP_MAX_AGENTS <= MDP_NT, "rollout prologue");
+  float pv[2] = {0.f, 0.f}, vv[2] = {0.f, 0.f}, er = 0.f;
+  const int er_r = tid / n, er_j = tid - er_r * n;
+  if (tid < MDP_R * n && er_r < nvalid) er = a.ep_rew[(int64_t)(e0 + er_r) * n + er_j];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = tid + u * MDP_NT, r = q / (2 * ne), c = q - r * 2 * ne;
+    if (q < MDP_R * 2 * ne && r < nvalid) {
+      pv[u] = a.pos[(int64_t)(e0 + r) * 2 * ne + c];
+      vv[u] = a.vel[(int64_t)(e0 + r) * 2 * ne + c];
     }
-    sp[r * 2 * MDP_MAX_ENT + c] = pv;
-    sv[r * 2 * MDP_MAX_ENT + c] = vv;
+  }
+  // (issued after the state loads: a register reused behind them made an
+  // earlier wait for this one)
+  const int64_t next_raw = gc->next, len_raw = gc->len;
+  const uint32_t step_raw = (uint32_t)gc->env_steps;
+  const int64_t ep_base_raw = gc->episodes;  // advanced only by this launch's last workgroup
+  if (tid < MDP_R * n) epr[er_r * MDP_MAX_AGENTS + er_j] = er;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = tid + u * MDP_NT, r = q / (2 * ne), c = q - r * 2 * ne;
+    if (q < MDP_R * 2 * ne) {
+      sp[r * 2 * MDP_MAX_ENT + c] = pv[u];
+      sv[r * 2 * MDP_MAX_ENT + c] = vv[u];
+    }
   }
   for (int q = tid; q < MDP_R * ldr; q += MDP_NT) rowt[q] = 0.f;
   __syncthreads();
-  int goal = 0;
   if (tid < MDP_R) {
-    goal = tid < nvalid ? a.goal[e0 + tid] : 0;
+    goal = (int)ctr_use((uint32_t)goal);
     for (int j = 0; j < n; ++j)
       env_obs(E, sp + tid * 2 * MDP_MAX_ENT, sv + tid * 2 * MDP_MAX_ENT, goal, j, rowt + tid * ldr + T.ag[j].obs_off);
   }
   __syncthreads();
 
+  MDP_STAMP(41);
   // policies: act_j = gumbel_softmax(actor_j(obs_j))  (MADDPGAgentTrainer.action)
   for (int j = 0; j < n; ++j) {
     const ADesc& aj = T.ag[j];
@@ -759,12 +794,13 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
           for (int k = 0; k < MDP_ACT_DIM; ++k)
             u[k] = tid < nvalid ? a.u_in[((int64_t)(e0 + tid) * n + j) * MDP_ACT_DIM + k] : 0.5f;
         } else {
-          uniforms5(a.seed, 0x10000u | (uint32_t)j, step, (uint32_t)(a.env_base + e0 + tid), u);
+          uniforms5(a.seed, 0x10000u | (uint32_t)j, ctr_use(step_raw), (uint32_t)(a.env_base + e0 + tid), u);
         }
         gumbel_softmax5(lg + tid * 8, u, dst);
       }
     }
     __syncthreads();
+    if (j < 4) MDP_STAMP(42 + j);
   }
 
   // physics, next obs, rewards, bookkeeping (one thread per env)
@@ -787,22 +823,23 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     const int e = e0 + tid;
     float tot = 0.f;
     for (int j = 0; j < n; ++j) {
-      const float r = a.ep_rew[(int64_t)e * n + j] + rew[j];
+      const float r = epr[tid * MDP_MAX_AGENTS + j] + rew[j];
+      epr[tid * MDP_MAX_AGENTS + j] = r;
       a.ep_rew[(int64_t)e * n + j] = r;
       tot += r;
     }
-    const int st = a.ep_step[e] + 1;
+    const int st = (int)ctr_use((uint32_t)ep_st) + 1;
     if (st >= E.max_ep_len) {  // terminal -> log episode, env.reset() (train.py:127-133)
       const uint32_t q = atomicAdd(&a.ctl->ep_pending, 1u);
-      const int64_t slot = ep_base + (a.eplog_by_env ? (int64_t)e : (int64_t)q);
+      const int64_t slot = ep_base_raw + (a.eplog_by_env ? (int64_t)e : (int64_t)q);
       float* lgp = a.eplog + (slot % a.eplog_cap) * (1 + n);
       lgp[0] = tot;
       for (int j = 0; j < n; ++j) {
-        lgp[1 + j] = a.ep_rew[(int64_t)e * n + j];
+        lgp[1 + j] = epr[tid * MDP_MAX_AGENTS + j];
         a.ep_rew[(int64_t)e * n + j] = 0.f;
       }
       int32_t g;
-      env_reset_one(E, a.seed, 0x20000u, step, (uint32_t)(a.env_base + e), p, v, &g);
+      env_reset_one(E, a.seed, 0x20000u, ctr_use(step_raw), (uint32_t)(a.env_base + e), p, v, &g);
       a.goal[e] = g;
       a.ep_step[e] = 0;
     } else {
@@ -810,12 +847,13 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     }
   }
   __syncthreads();
+  MDP_STAMP(46);
   // replay append of the 16 rows + env state store
   const int v4 = T.row_stride >> 2;
   for (int q = tid; q < nvalid * v4; q += MDP_NT) {
     const int r = q / v4, c4 = q - r * v4;
     const float* s = rowt + r * ldr + c4 * 4;
-    const int64_t dst = (next + e0 + r) % a.cap;
+    const int64_t dst = (next_raw + e0 + r) % a.cap;
     *reinterpret_cast<float4*>(a.replay + dst * T.row_stride + c4 * 4) = make_float4(s[0], s[1], s[2], s[3]);
   }
   for (int q = tid; q < nvalid * 2 * ne; q += MDP_NT) {
@@ -823,7 +861,8 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     a.pos[(int64_t)(e0 + r) * 2 * ne + c] = sp[r * 2 * MDP_MAX_ENT + c];
     a.vel[(int64_t)(e0 + r) * 2 * ne + c] = sv[r * 2 * MDP_MAX_ENT + c];
   }
-  rollout_finish(a, next, len);
+  MDP_STAMP(47);
+  rollout_finish(a, next_raw, len_raw);
 }
 
 // batched policy / critic evaluation for the facade (action, target_act, q_values)
@@ -993,3 +1032,10 @@ hipError_t mdp_launch_set_ring(Ctl* ctl, int64_t len, int64_t next, hipStream_t 
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
+
+#ifdef MDP_STAMPS
+// diagnostic build: stamps of this translation unit's kernels (k_rollout: 40..47)
+extern "C" int mdp_debug_stamps_k(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif
