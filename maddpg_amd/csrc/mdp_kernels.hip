@@ -136,6 +136,32 @@ __device__ inline void colsum_store(const float* X, int ldx, int ncols, float* _
   }
 }
 
+// The same forward at H = 64 with in <= 64 (one 64-deep weight chunk per
+// layer): every layer's fragments -- and the head's on wave 0 -- are requested
+// before the first MFMA, one memory round trip per net instead of one per
+// layer (the rollout ran three per agent).  Same chains and head as
+// mlp_fwd_tile<64>: bit-identical.
+__device__ inline void mlp_fwd_tile_pf64(const float* X, int ldx, int K, const float* P, const NDesc& nd, float* h1,
+                                         float* h2, int ldh, float* out, int ldo) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, kq = lane >> 4, col = wave * 16 + r;
+  float w1[MDP_KC], w2[MDP_KC], w3[16], b3 = 0.f;
+  load_wchunk(w1, P + nd.t[0].off, 64, col, 0, K, kq);
+  load_wchunk(w2, P + nd.t[2].off, 64, col, 0, 64, kq);
+  if (wave == 0) head_load<16>(w3, b3, P + nd.t[4].off, P + nd.t[5].off, nd.out);
+  const float b1 = P[nd.t[1].off + col], b2 = P[nd.t[3].off + col];
+  f32x4 acc = mfma_chunk(f32x4{0.f, 0.f, 0.f, 0.f}, w1, X, ldx, r, 0, K, kq);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h1[(kq * 4 + i) * ldh + col] = fmaxf(acc[i] + b1, 0.f);
+  __syncthreads();
+  acc = mfma_chunk(f32x4{0.f, 0.f, 0.f, 0.f}, w2, h1, ldh, r, 0, 64, kq);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h2[(kq * 4 + i) * ldh + col] = fmaxf(acc[i] + b2, 0.f);
+  __syncthreads();
+  if (wave == 0) head_acc<16>(w3, b3, h2, ldh, nd.out, out, ldo);
+  __syncthreads();
+}
+
 template <int H>
 __device__ inline void mlp_fwd_tile(const float* X, int ldx, int K, const float* P, const NDesc& nd, float* h1,
                                     float* h2, int ldh, float* out, int ldo) {
@@ -782,7 +808,12 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   // policies: act_j = gumbel_softmax(actor_j(obs_j))  (MADDPGAgentTrainer.action)
   for (int j = 0; j < n; ++j) {
     const ADesc& aj = T.ag[j];
-    if (!a.act_in) mlp_fwd_tile<H>(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
+    if (!a.act_in) {
+      if (H == 64 && MDP_NW == 4 && aj.obs_dim <= 4 * MDP_KC)
+        mlp_fwd_tile_pf64(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
+      else
+        mlp_fwd_tile<H>(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
+    }
     if (tid < MDP_R) {
       float* dst = rowt + tid * ldr + aj.act_off;
       if (a.act_in) {
