@@ -845,11 +845,13 @@ template <int KS>
 __device__ __forceinline__ void rf_load(f32x4 (&w)[KS], const float* __restrict__ W, int K) {
   const int lane = threadIdx.x & 63, r = lane & 15;
   const int kq = lane >> 4;
+  // Unconditional, clamped to row K - 1: rf_acc skips the k-steps past K (and
+  // zeroes the A operand of rows >= K).  A per-k-step branch merged the loaded
+  // value with a zero into one register, and the copy made the wave wait for
+  // the load right where it was issued (ISA: global_load_dwordx4 + vmcnt(0) +
+  // v_mov in rf_load<2>); the clamped extra loads hit the same row's lines.
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    w[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (4 * s < K) w[s] = ld4(W + min(4 * s + kq, K - 1) * MDP_RH + 4 * r);  // wave-uniform branch
-  }
+  for (int s = 0; s < KS; ++s) w[s] = ld4(W + min(4 * s + kq, K - 1) * MDP_RH + 4 * r);
 }
 
 // acc[t] += X[16][K] @ W (the fragments of rf_load); X in LDS; input rows >= K
