@@ -316,6 +316,10 @@ __device__ __forceinline__ void tile_dgrad_relu(const float* dY, int ldy, int N,
 // MFMA column tile (column r = lane & 15): every weight of the lane is requested
 // up front (one memory round trip), then KS = K/4 dependent MFMAs.  Replaces
 // the VALU heads whose k-loop waited on one global load per iteration.
+// K is a multiple of 4 (every caller passes H), so a k-step is either wholly
+// inside K or skipped, and columns r >= nout are computed but never stored: the
+// weight loads need no select.  (A select on the loaded value made the compiler
+// branch around each load and wait for it there, one round trip per k-step.)
 template <int KS>
 __device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const float* __restrict__ W,
                                           const float* __restrict__ b, int nout, float* out, int ldo) {
@@ -331,8 +335,7 @@ __device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const 
 #pragma unroll
       for (int s = 0; s < MDP_KC; ++s) {
         const int k = c0 + 4 * s + kq;
-        const float v = W[min(k, kmax) * nout + c];
-        w[s] = (r < nout && k < K) ? v : 0.f;
+        w[s] = W[min(k, kmax) * nout + c];
         x[s] = X[r * ldx + min(k, kmax)];
       }
 #pragma unroll
@@ -350,8 +353,7 @@ __device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const 
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k = 4 * s + kq;
-    const float v = W[min(k, kmax) * nout + c];
-    w[s] = (r < nout && k < K) ? v : 0.f;
+    w[s] = W[min(k, kmax) * nout + c];
   }
 #pragma unroll
   for (int s = 0; s < KS; ++s) x[s] = X[r * ldx + min(4 * s + kq, kmax)];

@@ -697,6 +697,11 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     }
     __syncthreads();
   }
+  // the dq * W3 backward below reads one W3 column per thread (the block is a
+  // multiple of H wide): requested here, ahead of the TD-error phase, instead
+  // of one dependent load per row pass after it
+  static_assert(MDP_GEN_THREADS % H == 0, "d2 pass: fixed column per thread");
+  const float w3h = a.theta[nd.t[4].off + tid % H];
   if (wave == 0) {
     const float* P = a.target;
     if constexpr (H / 4 <= 32) head_acc<HKS>(thw, thb, hB, ldh, 1, lg, 8);
@@ -736,7 +741,6 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
 
   // backward through the critic (tf.gradients of q_loss w.r.t. q_func vars)
   float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
-  const float* W3 = a.theta + nd.t[4].off;
   float* d2 = hA;
   float* d1 = hB;
   if (tid < H) {
@@ -749,10 +753,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     for (int r = 0; r < MDP_R; ++r) s += dq[r];
     slab[nd.t[5].off] = s;
   }
-  for (int e = tid; e < MDP_R * H; e += blockDim.x) {
-    const int r = e / H, h = e - r * H;
-    d2[r * ldh + h] = h2c[r * ldh + h] > 0.f ? dq[r] * W3[h] : 0.f;
-  }
+  for (int r = tid / H, h = tid % H; r < MDP_R; r += MDP_GEN_THREADS / H)
+    d2[r * ldh + h] = h2c[r * ldh + h] > 0.f ? dq[r] * w3h : 0.f;
   __syncthreads();
   MDP_STAMP(4);
   // dh1 tiles then dW2 tiles, dealt over all waves
@@ -863,6 +865,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   __syncthreads();
   MDP_STAMP(37);
   float qw[HKS], qb = 0.f;  // the critic head's fragments (q), issued ahead on an idle wave
+  const float w3h = P[nc.t[4].off + tid % H];  // d2 pass below: one W3c column per thread
   if (wave < NT) {
     fwd_tile_pf<true>(h1c, ldh, 0, H, P + nc.t[2].off, P + nc.t[3].off, H, nullptr, 0, h2c, ldh, wave, pf);
     pf_load_t(pft, P + nc.t[2].off, H, wave);  // dh1c = d2 W2c^T
@@ -875,11 +878,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   // waits for the next phase, on a wave the dh1c tiles leave idle
   const bool q_late = NT < nw;
   if (!q_late && wave == 0) head_mfma<H / 4>(h2c, ldh, H, P + nc.t[4].off, P + nc.t[5].off, 1, qv, 8);
-  const float* W3c = P + nc.t[4].off;
-  for (int e = tid; e < MDP_R * H; e += blockDim.x) {
-    const int r = e / H, h = e - r * H;
-    d2[r * ldh + h] = (r < nvalid && h2c[r * ldh + h] > 0.f) ? a.neg_inv_b * W3c[h] : 0.f;
-  }
+  for (int r = tid / H, h = tid % H; r < MDP_R; r += MDP_GEN_THREADS / H)
+    d2[r * ldh + h] = (r < nvalid && h2c[r * ldh + h] > 0.f) ? a.neg_inv_b * w3h : 0.f;
   __syncthreads();
   MDP_STAMP(39);
   // dh1c = d2 @ W2c^T masked by h1c > 0

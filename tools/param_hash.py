@@ -1,5 +1,5 @@
 """Diagnostic: sha256 of every parameter region after three update rounds on
-fixed data (S2 at B=1024 and tag N=6 at H=128, B=1000), to check that a
+fixed data (S2 at B=1024, tag N=6 at H=128, B=1000, and H=256), to check that a
 scheduling change is bit-identical against another build:
     python tools/param_hash.py; MDP_LIB=maddpg_amd/libmaddpg_hip_ref.so python tools/param_hash.py"""
 import hashlib
@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from maddpg_amd.engine import Engine  # noqa: E402
 
-for dims, H, B in (([18, 18, 18], 64, 1024), ([22, 22, 22, 22, 20, 20], 128, 1000)):
+for dims, H, B in (([18, 18, 18], 64, 1024), ([22, 22, 22, 22, 20, 20], 128, 1000), ([16, 16], 256, 512)):
     g = torch.Generator().manual_seed(5)
     eng = Engine(dims, num_units=H, batch_size=B, capacity=30000)
     eng.add_rows(torch.rand(eng.capacity, eng.row_stride, generator=g))
