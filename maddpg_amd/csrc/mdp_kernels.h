@@ -328,7 +328,7 @@ inline bool grads_r_ok(const Topo& t, int agent) {
 inline int lds_rollout_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), ldh = t.H + 1;
   return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8) + 2 * mdp_r4(R * 2 * MDP_MAX_ENT) +
-              mdp_r4(R * 3 * MDP_MAX_ENT) + mdp_r4(R * MDP_MAX_AGENTS));
+              mdp_r4(R * 3 * MDP_MAX_ENT) + mdp_r4(R * MDP_MAX_AGENTS) + mdp_r4(R));
 }
 inline int lds_eval_bytes(int in, int H) {
   const int R = 16, ldx = mdp_ld(in), ldh = H + 1;

@@ -136,29 +136,54 @@ __device__ inline void colsum_store(const float* X, int ldx, int ncols, float* _
   }
 }
 
-// The same forward at H = 64 with in <= 64 (one 64-deep weight chunk per
-// layer): every layer's fragments -- and the head's on wave 0 -- are requested
-// before the first MFMA, one memory round trip per net instead of one per
-// layer (the rollout ran three per agent).  Same chains and head as
-// mlp_fwd_tile<64>: bit-identical.
-__device__ inline void mlp_fwd_tile_pf64(const float* X, int ldx, int K, const float* P, const NDesc& nd, float* h1,
-                                         float* h2, int ldh, float* out, int ldo) {
+// mlp_fwd_tile for H = 64 / 128 with in <= 64 (one 64-deep weight chunk for
+// layer 1): every fragment of the wave's column tiles -- both layers, and the
+// head's on wave 0 -- is requested before the first MFMA, one memory round
+// trip per net instead of one per layer and tile (at H = 128 the rollout ran
+// about seven per agent).  Same tiles, chunk order and head as mlp_fwd_tile<H>:
+// bit-identical.
+template <int H>
+__device__ inline void mlp_fwd_tile_pf(const float* X, int ldx, int K, const float* P, const NDesc& nd, float* h1,
+                                       float* h2, int ldh, float* out, int ldo) {
+  static_assert(H == 64 || H == 128, "register budget: H <= 128");
+  constexpr int TW = H / (16 * MDP_NW);  // column tiles per wave (tile_fwd deals nt = wave + t * MDP_NW)
+  constexpr int KC2 = H / (4 * MDP_KC);  // 64-deep chunks of layer 2
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 15, kq = lane >> 4, col = wave * 16 + r;
-  float w1[MDP_KC], w2[MDP_KC], w3[16], b3 = 0.f;
-  load_wchunk(w1, P + nd.t[0].off, 64, col, 0, K, kq);
-  load_wchunk(w2, P + nd.t[2].off, 64, col, 0, 64, kq);
-  if (wave == 0) head_load<16>(w3, b3, P + nd.t[4].off, P + nd.t[5].off, nd.out);
-  const float b1 = P[nd.t[1].off + col], b2 = P[nd.t[3].off + col];
-  f32x4 acc = mfma_chunk(f32x4{0.f, 0.f, 0.f, 0.f}, w1, X, ldx, r, 0, K, kq);
+  const int r = lane & 15, kq = lane >> 4;
+  float w1[TW][MDP_KC], w2[TW][KC2][MDP_KC], w3[H / 4], b3 = 0.f, b1[TW], b2[TW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) h1[(kq * 4 + i) * ldh + col] = fmaxf(acc[i] + b1, 0.f);
-  __syncthreads();
-  acc = mfma_chunk(f32x4{0.f, 0.f, 0.f, 0.f}, w2, h1, ldh, r, 0, 64, kq);
+  for (int t = 0; t < TW; ++t) {
+    const int col = (wave + t * MDP_NW) * 16 + r;
+    load_wchunk(w1[t], P + nd.t[0].off, H, col, 0, K, kq);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) h2[(kq * 4 + i) * ldh + col] = fmaxf(acc[i] + b2, 0.f);
+    for (int c = 0; c < KC2; ++c) load_wchunk(w2[t][c], P + nd.t[2].off, H, col, c * 4 * MDP_KC, H, kq);
+  }
+  if (wave == 0) head_load<H / 4>(w3, b3, P + nd.t[4].off, P + nd.t[5].off, nd.out);
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int col = (wave + t * MDP_NW) * 16 + r;
+    b1[t] = P[nd.t[1].off + col];
+    b2[t] = P[nd.t[3].off + col];
+  }
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int col = (wave + t * MDP_NW) * 16 + r;
+    const f32x4 acc = mfma_chunk(f32x4{0.f, 0.f, 0.f, 0.f}, w1[t], X, ldx, r, 0, K, kq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h1[(kq * 4 + i) * ldh + col] = fmaxf(acc[i] + b1[t], 0.f);
+  }
   __syncthreads();
-  if (wave == 0) head_acc<16>(w3, b3, h2, ldh, nd.out, out, ldo);
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int col = (wave + t * MDP_NW) * 16 + r;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC2; ++c) acc = mfma_chunk(acc, w2[t][c], h1, ldh, r, c * 4 * MDP_KC, H, kq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h2[(kq * 4 + i) * ldh + col] = fmaxf(acc[i] + b2[t], 0.f);
+  }
+  __syncthreads();
+  if (wave == 0) head_acc<H / 4>(w3, b3, h2, ldh, nd.out, out, ldo);
   __syncthreads();
 }
 
@@ -573,60 +598,70 @@ __device__ inline void env_bench(const EnvDesc& E, const float* p, int goal, flo
   }
 }
 
-// World.step (core.py): action force, pairwise soft contact, damping,
-// integration with max_speed clamp.  p, v: [ne][2] of one env (in place).
-// f: this env's force scratch [3][MDP_MAX_ENT] in LDS (fx, fy, has) -- as
-// private arrays with runtime indices they lived in scratch memory, a
-// read-modify-write round trip through the vector memory path per contact
-__device__ inline void env_physics(const EnvDesc& E, float* p, float* v, const float* act /*[n][5]*/, float* f) {
+// World.step (core.py) for a tile of envs: action force, pairwise soft contact,
+// damping, integration with max_speed clamp.  One thread per (env, entity)
+// (one thread per env ran 33 of the 98 us S5 rollout): the force on entity e is
+// summed over its contacts in the order the pair loop of core.py adds them --
+// pairs (o, e) for o < e, then (e, o) for o > e -- with each pair's force
+// computed in the same (a < b) orientation, so the result is bit-identical to
+// the one-thread-per-env loop (and the oracle's); then damping and integration,
+// after a barrier (they move the positions the contacts read).  sp / sv: the
+// tile's [R][2 MDP_MAX_ENT] state; f: [R][3 MDP_MAX_ENT] force scratch; act:
+// row r's actions at act + r * ldr.  Every thread of the workgroup calls it.
+__device__ inline void env_physics_tile(const EnvDesc& E, float* sp, float* sv, const float* act, int ldr, float* f,
+                                        int nvalid) {
   const int n = E.n_agents, ne = E.n_agents + E.n_landmarks;
-  float* fx = f;
-  float* fy = f + MDP_MAX_ENT;
-  float* has = f + 2 * MDP_MAX_ENT;
-  for (int e = 0; e < ne; ++e) {
-    fx[e] = 0.f;
-    fy[e] = 0.f;
-    has[e] = 0.f;
-  }
-  for (int i = 0; i < n; ++i) {  // environment._set_action, discrete action space
-    const float* a = act + i * MDP_ACT_DIM;
-    fx[i] = (a[1] - a[2]) * E.accel[i];
-    fy[i] = (a[3] - a[4]) * E.accel[i];
-    has[i] = 1.f;
-  }
   const float k = 1e-3f;  // contact_margin
-  for (int a = 0; a < ne; ++a) {
-    if (!E.collide[a]) continue;
-    for (int b = a + 1; b < ne; ++b) {
-      if (!E.collide[b]) continue;
-      const float dx = p[2 * a] - p[2 * b], dy = p[2 * a + 1] - p[2 * b + 1];
-      const float dist = sqrtf(dx * dx + dy * dy);
-      const float dmin = E.size[a] + E.size[b];
-      const float pen = softplus_f(-(dist - dmin) / k) * k;
-      const float sx = 1e2f * dx / dist * pen, sy = 1e2f * dy / dist * pen;
-      if (E.movable[a]) {
-        fx[a] = sx + fx[a];
-        fy[a] = sy + fy[a];
-        has[a] = 1.f;
-      }
-      if (E.movable[b]) {
-        fx[b] = -sx + fx[b];
-        fy[b] = -sy + fy[b];
-        has[b] = 1.f;
+  for (int q = threadIdx.x; q < nvalid * ne; q += MDP_NT) {
+    const int r = q / ne, e = q - r * ne;
+    const float* p = sp + r * 2 * MDP_MAX_ENT;
+    float fx = 0.f, fy = 0.f, has = 0.f;
+    if (e < n) {  // environment._set_action, discrete action space
+      const float* a = act + r * ldr + e * MDP_ACT_DIM;
+      fx = (a[1] - a[2]) * E.accel[e];
+      fy = (a[3] - a[4]) * E.accel[e];
+      has = 1.f;
+    }
+    if (E.collide[e] && E.movable[e]) {
+      for (int o = 0; o < ne; ++o) {
+        if (o == e || !E.collide[o]) continue;
+        const int a = min(o, e), b = max(o, e);
+        const float dx = p[2 * a] - p[2 * b], dy = p[2 * a + 1] - p[2 * b + 1];
+        const float dist = sqrtf(dx * dx + dy * dy);
+        const float dmin = E.size[a] + E.size[b];
+        const float pen = softplus_f(-(dist - dmin) / k) * k;
+        const float sx = 1e2f * dx / dist * pen, sy = 1e2f * dy / dist * pen;
+        if (e == a) {
+          fx = sx + fx;
+          fy = sy + fy;
+        } else {
+          fx = -sx + fx;
+          fy = -sy + fy;
+        }
+        has = 1.f;
       }
     }
+    float* fr = f + r * 3 * MDP_MAX_ENT;
+    fr[e] = fx;
+    fr[MDP_MAX_ENT + e] = fy;
+    fr[2 * MDP_MAX_ENT + e] = has;
   }
-  for (int e = 0; e < ne; ++e) {
+  __syncthreads();
+  for (int q = threadIdx.x; q < nvalid * ne; q += MDP_NT) {
+    const int r = q / ne, e = q - r * ne;
     if (!E.movable[e]) continue;
+    float* p = sp + r * 2 * MDP_MAX_ENT;
+    float* v = sv + r * 2 * MDP_MAX_ENT;
+    const float* fr = f + r * 3 * MDP_MAX_ENT;
     float vx = v[2 * e] * (1.f - 0.25f), vy = v[2 * e + 1] * (1.f - 0.25f);
-    if (has[e] != 0.f) {
-      vx += (fx[e] / 1.f) * 0.1f;
-      vy += (fy[e] / 1.f) * 0.1f;
+    if (fr[2 * MDP_MAX_ENT + e] != 0.f) {
+      vx += (fr[e] / 1.f) * 0.1f;
+      vy += (fr[MDP_MAX_ENT + e] / 1.f) * 0.1f;
     }
     const float ms = E.max_speed[e];
     if (ms >= 0.f) {
-      const float sp = sqrtf(vx * vx + vy * vy);
-      if (sp > ms) {
+      const float spd = sqrtf(vx * vx + vy * vy);
+      if (spd > ms) {
         const float s = sqrtf(vx * vx + vy * vy);
         vx = vx / s * ms;
         vy = vy / s * ms;
@@ -637,6 +672,7 @@ __device__ inline void env_physics(const EnvDesc& E, float* p, float* v, const f
     p[2 * e] += vx * 0.1f;
     p[2 * e + 1] += vy * 0.1f;
   }
+  __syncthreads();
 }
 
 // reset_world of one env from Philox uniforms
@@ -732,6 +768,7 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   float* sv = cv.take(MDP_R * 2 * MDP_MAX_ENT);
   float* sfo = cv.take(MDP_R * 3 * MDP_MAX_ENT);  // per-env force scratch of env_physics
   float* epr = cv.take(MDP_R * MDP_MAX_AGENTS);    // the envs' running episode rewards
+  int* sgoal = reinterpret_cast<int*>(cv.take(MDP_R));  // the envs' goal landmarks
 
   const int tid = threadIdx.x;
   // with a draw workgroup it is block 0 (dispatched first: at tag6 B=4096 the
@@ -796,11 +833,13 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     }
   }
   for (int q = tid; q < MDP_R * ldr; q += MDP_NT) rowt[q] = 0.f;
+  if (tid < MDP_R) sgoal[tid] = (int)ctr_use((uint32_t)goal);
   __syncthreads();
-  if (tid < MDP_R) {
-    goal = (int)ctr_use((uint32_t)goal);
-    for (int j = 0; j < n; ++j)
-      env_obs(E, sp + tid * 2 * MDP_MAX_ENT, sv + tid * 2 * MDP_MAX_ENT, goal, j, rowt + tid * ldr + T.ag[j].obs_off);
+  // observations, one thread per (env, agent)
+  static_assert(MDP_R * MDP_MAX_AGENTS <= MDP_NT, "rollout obs: one pass");
+  if (tid < MDP_R * n) {
+    const int r = tid / n, j = tid - r * n;
+    env_obs(E, sp + r * 2 * MDP_MAX_ENT, sv + r * 2 * MDP_MAX_ENT, sgoal[r], j, rowt + r * ldr + T.ag[j].obs_off);
   }
   __syncthreads();
 
@@ -809,10 +848,16 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   for (int j = 0; j < n; ++j) {
     const ADesc& aj = T.ag[j];
     if (!a.act_in) {
-      if (H == 64 && MDP_NW == 4 && aj.obs_dim <= 4 * MDP_KC)
-        mlp_fwd_tile_pf64(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
-      else
-        mlp_fwd_tile<H>(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
+      bool pf = false;
+      // (H = 64 only: at H = 128 the fragments take the kernel to 256 VGPRs, one
+      // workgroup per CU, for 0.3 of the 6 us per agent)
+      if constexpr (H == 64 && MDP_NW == 4) {
+        if (aj.obs_dim <= 4 * MDP_KC) {
+          mlp_fwd_tile_pf<H>(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
+          pf = true;
+        }
+      }
+      if (!pf) mlp_fwd_tile<H>(rowt + aj.obs_off, ldr, aj.obs_dim, a.theta, aj.actor, h1, h2, ldh, lg, 8);
     }
     if (tid < MDP_R) {
       float* dst = rowt + tid * ldr + aj.act_off;
@@ -834,23 +879,20 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     if (j < 4) MDP_STAMP(42 + j);
   }
 
-  // physics, next obs, rewards, bookkeeping (one thread per env)
+  // physics (one thread per (env, entity)), then rewards and bookkeeping (one
+  // thread per env, wave 0) beside the next observations (one thread per
+  // (env, agent), the other waves); terminal envs reset after both
+  env_physics_tile(E, sp, sv, rowt + T.ag[0].act_off, ldr, sfo, nvalid);
+  bool term = false;
   if (tid < nvalid) {
-    float* p = sp + tid * 2 * MDP_MAX_ENT;
-    float* v = sv + tid * 2 * MDP_MAX_ENT;
+    const float* p = sp + tid * 2 * MDP_MAX_ENT;
     float* row = rowt + tid * ldr;
-    // the row's actions act_0 .. act_{n-1} and rewards rew_0 .. rew_{n-1} are
-    // contiguous (mdp_topo.h): read and written in place, not through private
-    // arrays (scratch memory)
-    env_physics(E, p, v, row + T.ag[0].act_off, sfo + tid * 3 * MDP_MAX_ENT);
+    // the row's rewards rew_0 .. rew_{n-1} are contiguous (mdp_topo.h): written
+    // in place, not through a private array (scratch memory)
     float* rew = row + T.ag[0].rew_off;
     env_reward(E, p, goal, rew);
     if (a.bench) env_bench(E, p, goal, a.bench + (int64_t)(e0 + tid) * n * MDP_BENCH_W);
-    for (int j = 0; j < n; ++j) {
-      env_obs(E, p, v, goal, j, row + T.ag[j].nobs_off);
-      row[T.ag[j].rew_off] = rew[j];
-      row[T.ag[j].done_off] = 0.f;  // done_callback is None (environment.py _get_done)
-    }
+    for (int j = 0; j < n; ++j) row[T.ag[j].done_off] = 0.f;  // done_callback is None (environment.py _get_done)
     const int e = e0 + tid;
     float tot = 0.f;
     for (int j = 0; j < n; ++j) {
@@ -860,7 +902,8 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
       tot += r;
     }
     const int st = (int)ctr_use((uint32_t)ep_st) + 1;
-    if (st >= E.max_ep_len) {  // terminal -> log episode, env.reset() (train.py:127-133)
+    term = st >= E.max_ep_len;
+    if (term) {  // terminal -> log episode, env.reset() (train.py:127-133)
       const uint32_t q = atomicAdd(&a.ctl->ep_pending, 1u);
       const int64_t slot = ep_base_raw + (a.eplog_by_env ? (int64_t)e : (int64_t)q);
       float* lgp = a.eplog + (slot % a.eplog_cap) * (1 + n);
@@ -869,13 +912,22 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
         lgp[1 + j] = epr[tid * MDP_MAX_AGENTS + j];
         a.ep_rew[(int64_t)e * n + j] = 0.f;
       }
-      int32_t g;
-      env_reset_one(E, a.seed, 0x20000u, ctr_use(step_raw), (uint32_t)(a.env_base + e), p, v, &g);
-      a.goal[e] = g;
-      a.ep_step[e] = 0;
     } else {
       a.ep_step[e] = st;
     }
+  } else if (tid >= 64 && tid - 64 < nvalid * n) {
+    const int q = tid - 64, r = q / n, j = q - r * n;
+    env_obs(E, sp + r * 2 * MDP_MAX_ENT, sv + r * 2 * MDP_MAX_ENT, sgoal[r], j, rowt + r * ldr + T.ag[j].nobs_off);
+  }
+  static_assert(64 + MDP_R * MDP_MAX_AGENTS <= MDP_NT, "rollout obs': one pass on waves 1..");
+  __syncthreads();
+  if (term) {
+    const int e = e0 + tid;
+    int32_t g;
+    env_reset_one(E, a.seed, 0x20000u, ctr_use(step_raw), (uint32_t)(a.env_base + e), sp + tid * 2 * MDP_MAX_ENT,
+                  sv + tid * 2 * MDP_MAX_ENT, &g);
+    a.goal[e] = g;
+    a.ep_step[e] = 0;
   }
   __syncthreads();
   MDP_STAMP(46);

@@ -24,3 +24,16 @@ for dims, H, B in (([18, 18, 18], 64, 1024), ([22, 22, 22, 22, 20, 20], 128, 100
     for reg in ("theta", "target", "adam_m", "adam_v"):
         h.update(eng.region(reg).cpu().numpy().tobytes())
     print(f"dims={dims} H={H} B={B}: {h.hexdigest()[:16]}")
+
+# the device rollout: replay rows and env state after a few vector env steps
+for dims, H, scn, na in (([18, 18, 18], 64, "simple_spread", 0), ([22, 22, 22, 22, 20, 20], 128, "simple_tag", 4),
+                         ([18, 18, 18], 256, "simple_spread", 0)):
+    eng = Engine(dims, num_units=H, batch_size=256, capacity=8192, num_envs=1000, scenario=scn, num_adversaries=na)
+    eng.init_params(3)
+    eng.env_reset()
+    for _ in range(6):
+        eng.env_step()
+    eng.synchronize()
+    h = hashlib.sha256()
+    h.update(eng.region("replay").cpu().numpy().tobytes())
+    print(f"rollout {scn} H={H}: {h.hexdigest()[:16]}")

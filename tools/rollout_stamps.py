@@ -1,7 +1,8 @@
 """Diagnostic: phase timings of k_rollout workgroup 0 (S2, E=1024) from the
 -DMDP_STAMPS build:
     make -C maddpg_amd/csrc stamps
-    MDP_LIB=maddpg_amd/libmaddpg_hip_stamps.so python tools/rollout_stamps.py"""
+    MDP_LIB=maddpg_amd/libmaddpg_hip_stamps.so python tools/rollout_stamps.py [tag6]
+(tag6: simple_tag N=6, H=128, E=4096 -- the S5 rollout)"""
 import ctypes
 import os
 import sys
@@ -13,7 +14,11 @@ from maddpg_amd import _lib  # noqa: E402
 from maddpg_amd.engine import Engine  # noqa: E402
 
 assert "stamps" in _lib.LIB_PATH
-eng = Engine([18, 18, 18], batch_size=1024, capacity=60000, num_envs=1024, scenario="simple_spread")
+if sys.argv[1:] == ["tag6"]:
+    eng = Engine([22, 22, 22, 22, 20, 20], num_units=128, batch_size=4096, capacity=60000, num_envs=4096,
+                 scenario="simple_tag", num_adversaries=4)
+else:
+    eng = Engine([18, 18, 18], batch_size=1024, capacity=60000, num_envs=1024, scenario="simple_spread")
 eng.init_params(0)
 eng.env_reset()
 for _ in range(8):
@@ -25,7 +30,7 @@ fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 64)()
 fn(buf, 64)
 st = np.array(buf[:], dtype=np.int64)
-names = [(41, "state load + obs"), (42, "agent 0 forward + sample"), (43, "agent 1"), (44, "agent 2"),
+names = [(41, "state load + obs"), (42, "agent 0 forward + sample"), (43, "agent 1"), (44, "agent 2"), (45, "agent 3"),
          (46, "physics, reward, obs', episode"), (47, "replay append + state store")]
 prev = st[40]
 for i, nm in names:
