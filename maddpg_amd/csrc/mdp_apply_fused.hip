@@ -185,7 +185,9 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     // Adam state of the chunk, requested with the partial-gradient loads
     f32x4 m4 = {0.f, 0.f, 0.f, 0.f}, v4 = m4, th4 = m4, tg4 = m4;
     const float b1p = a.beta[0], b2p = a.beta[1];  // this step's powers (advanced at the end)
-    const uint32_t ep = f.phase == 3 ? f.xstep[0] + 1u : 0u;  // exchange epoch (advanced at the end)
+    // exchange epoch (advanced at the end); kept opaque until the exchange --
+    // the +1 here made the compiler wait for the load in front of the partials
+    const uint32_t ep_raw = f.phase == 3 ? f.xstep[0] : 0u;
     const uint32_t nep = f.sync_ctr[7 * 32] + 1u;                // norm-handshake epoch (advanced at the end)
     // a fault recorded by an earlier launch, read with the first loads (not
     // after the handshake, where its round trip would sit in front of Adam)
@@ -235,7 +237,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
 #pragma unroll
       for (int q = 1; q < 16; ++q) g += red[q][col];
       MDP_STAMP(34);
-      if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ep);
+      if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ctr_use(ep_raw) + 1u);
       double ss = 0.0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
