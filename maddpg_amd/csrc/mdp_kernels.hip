@@ -790,7 +790,9 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     // MT state is untouched by the env workgroups, and the length is the one
     // the last workgroup below will store (every workgroup read ctl->len
     // before arriving at the ticket)
+    MDP_STAMP(48);
     make_index_block<MDP_NT>(a.ctl, a.pf_count, a.pf_out, (uint32_t)(len + a.E < a.cap ? len + a.E : a.cap));
+    MDP_STAMP(49);
     rollout_finish(a, next, len);
     return;
   }
