@@ -356,8 +356,10 @@ __device__ __forceinline__ void pf_load_t(f32x4 (&wa)[4], const float* __restric
   load_wchunk_tc(wa, W, N, nt * 16 + (lane & 15), 0, lane >> 4);
 }
 // Y tile = act([init +] X[:, k0:K] W[k0:K, :] + b); init (raw accumulator of the
-// rows before k0, same MFMA k order as one chain) may be null
-template <bool RELU>
+// rows before k0, same MFMA k order as one chain) may be null.  DEEP: with at
+// most three 64-deep chunks, the second and third are requested together at
+// entry (one round trip after the prefetched first, not two); same chain.
+template <bool RELU, bool DEEP = false>
 __device__ __forceinline__ void fwd_tile_pf(const float* X, int ldx, int k0, int K, const float* __restrict__ W,
                                             const float* __restrict__ b, int N, const float* init, int ldi, float* Y,
                                             int ldy, int nt, float (&wa)[MDP_KC]) {
@@ -370,6 +372,15 @@ __device__ __forceinline__ void fwd_tile_pf(const float* X, int ldx, int k0, int
   }
   const float bias = b[col];
   float wb[MDP_KC];
+  constexpr int D = 4 * MDP_KC;
+  if (DEEP && K - k0 <= 3 * D) {
+    float wc[MDP_KC];
+    if (k0 + D < K) load_wchunk(wb, W, N, col, k0 + D, K, kq);
+    if (k0 + 2 * D < K) load_wchunk(wc, W, N, col, k0 + 2 * D, K, kq);
+    acc = mfma_chunk(acc, wa, X, ldx, r, k0, K, kq);
+    if (k0 + D < K) acc = mfma_chunk(acc, wb, X, ldx, r, k0 + D, K, kq);
+    if (k0 + 2 * D < K) acc = mfma_chunk(acc, wc, X, ldx, r, k0 + 2 * D, K, kq);
+  } else
   for (int c0 = k0; c0 < K; c0 += 4 * MDP_KC) {
     const bool more = c0 + 4 * MDP_KC < K;
     if (more) load_wchunk(wb, W, N, col, c0 + 4 * MDP_KC, K, kq);
@@ -859,7 +870,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   MDP_STAMP(36);
   // critic (post-step weights) forward
   if (wave < NT) {
-    fwd_tile_pf<true>(x, ldc, 0, cin, P + nc.t[0].off, P + nc.t[1].off, H, nullptr, 0, h1c, ldh, wave, pf);
+    fwd_tile_pf<true, true>(x, ldc, 0, cin, P + nc.t[0].off, P + nc.t[1].off, H, nullptr, 0, h1c, ldh, wave, pf);
     pf_load(pf, P + nc.t[2].off, H, wave, 0, H);
   }
   __syncthreads();
