@@ -529,8 +529,11 @@ def test_fused_reduce_apply_matches_two_kernel_path(monkeypatch):
 
 
 # --------------------------------------------------------------------- env
+# ("simple_spread", 8, 0): the maximum sizes -- 8 agents (MDP_MAX_AGENTS) and 16
+# entities (MDP_MAX_ENT), every thread of the rollout tile in the per-(env,
+# entity) physics and 128 of them in the per-(env, agent) observations
 SCENARIOS = [("simple", 1, 0), ("simple_spread", 3, 0), ("simple_adversary", 3, 1),
-             ("simple_tag", 4, 3), ("simple_tag", 6, 4)]
+             ("simple_tag", 4, 3), ("simple_tag", 6, 4), ("simple_spread", 8, 0)]
 
 
 def _oracle_scn(name, n, na):
