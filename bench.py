@@ -203,9 +203,9 @@ def configs2_per_gpu(args, steps=12, warmup=3):
     4096 env copies, batch 1024, the same cadence (41 update rounds per vector
     step); the multi-GPU runs use this E per rank"""
     E = 4096
-    r = VecRunner(args.scenario, E, n_agents=args.num_agents, scenario_adversaries=args.scenario_adversaries,
-                  num_adversaries=args.num_adversaries, good_policy=args.good_policy, adv_policy=args.adv_policy,
-                  batch_size=args.batch_size, num_units=args.num_units, seed=args.seed + 1,
+    # pinned to BASELINE configs[2] (simple_spread N=3, maddpg policies,
+    # 64 units), whatever --scenario the main line ran
+    r = VecRunner("simple_spread", E, n_agents=3, batch_size=args.batch_size, num_units=64, seed=args.seed + 1,
                   train_every=args.train_every)
     r.prefill()
     for _ in range(warmup):
@@ -287,6 +287,9 @@ def main():
         one_step()
     r.synchronize()
 
+    xgmi = world > 1 and getattr(r, "dp_kind", None) == "native-xgmi"
+    if xgmi:
+        eng.dp_exchange_stats(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -308,7 +311,10 @@ def main():
     # keeps every rank's weights, targets, Adam moments and beta powers equal).
     # At N=1 the same fields describe the single replica (no communicator).
     r.synchronize()
-    info = {"ms_per_step": round(dt_local / args.steps * 1e3, 4), "checksum": eng.param_checksum()}
+    info = {"ms_per_step": round(dt_local / args.steps * 1e3, 4), "checksum": eng.param_checksum(),
+            "rounds": rounds}
+    if xgmi:   # in-kernel stamps of the timed region's exchanges (graph replays)
+        info["xgmi_wait"] = eng.dp_exchange_stats(reset=True)
     if world > 1:
         info["dp"] = eng.dp_info() if getattr(r, "native_dp", False) else {"kind": r.dp_kind, "ranks": world}
         allinfo = [None] * world
@@ -336,6 +342,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ro_dt = float(t.item())
     rollout_only = args.num_envs * ro_steps * world / ro_dt
+    ro_ms_local = ro_dt / ro_steps * 1e3
     # Kernel timing pass: the same workload again with a HIP event pair around
     # every launch of every kernel kind on the engine stream (this forces the
     # eager launch path; the timed region above replays the captured round graph).
@@ -348,6 +355,31 @@ def main():
     per_kind = {k: eng.prof_read(k) for k in kinds}
     for k in kinds:
         eng.prof_enable(k, False)
+    if world > 1:
+        # the first multi-GPU run diagnoses itself: per rank, what one gradient
+        # exchange costs and the share of an update round spent in exchanges
+        # (strict: 2N per round, one per optimizer step; throughput: one)
+        ex_per_round = 1 if args.update_mode == "throughput" else 2 * r.n
+        rps = info["rounds"] / args.steps if args.steps else 0.0
+        round_us = ((info["ms_per_step"] - ro_ms_local) * 1e3 / rps) if rps else None
+        ex = {"kind": r.dp_kind, "exchanges_per_round": ex_per_round,
+              "round_us": round(round_us, 3) if round_us else None}
+        if xgmi:
+            w = info["xgmi_wait"]
+            ex.update(source="in-kernel s_memrealtime: chunk stores -> every peer's chunk arrived",
+                      per_exchange_us=round(w["mean_us"], 3), longest_wait_us=round(w["max_us"], 3),
+                      chunk_exchanges=w["chunk_exchanges"])
+        elif per_kind.get("allreduce", (0, 0))[1]:
+            ms_ar, n_ar = per_kind["allreduce"]
+            ex.update(source="HIP events around each ncclAllReduce (kernel pass, eager)",
+                      per_exchange_us=round((ms_ar / n_ar - event_overhead_ms(eng.stream)) * 1e3, 3),
+                      allreduces_timed=n_ar)
+        if ex.get("per_exchange_us") is not None and round_us:
+            ex["wait_us_per_round"] = round(ex["per_exchange_us"] * ex_per_round, 3)
+            ex["wait_fraction_of_round"] = round(ex["wait_us_per_round"] / round_us, 4)
+        exall = [None] * world
+        dist.all_gather_object(exall, ex)
+        dp_check["exchange_per_rank"] = exall
     # the dominant kernel among those with a roofline model (the gradient launch
     # pair: MFMA; rollout, optimizer step: HBM)
     if per_kind["critic_grad"][1] and per_kind["critic_grad"][1] == per_kind["actor_grad"][1]:
@@ -476,7 +508,8 @@ def main():
             "roofline": roof,
             "throughput_mode": tp_fig,
         }
-        if world == 1 and not args.no_configs2 and args.num_envs != 4096:
+        if (world == 1 and not args.no_configs2 and
+                not (args.scenario == "simple_spread" and r.n == 3 and args.num_envs == 4096)):
             out["configs2_per_gpu"] = configs2_per_gpu(args)
         if world == 1 and not args.no_gather_stage:
             out["gather_stage"] = gather_stage(r.spec.obs_dims)

@@ -35,7 +35,7 @@ extern "C" {
 #define MDP_MAX_AGENTS 8
 #define MDP_ACT_DIM 5          /* MPE Discrete(dim_p*2+1) action spaces */
 #define MDP_MAX_UNITS 256      /* largest --num-units (train.py:24) */
-#define MDP_ABI_VERSION 2
+#define MDP_ABI_VERSION 3
 
 enum mdp_scenario {
     MDP_SCN_NONE = 0,          /* trainer only (no device env) */
@@ -81,6 +81,7 @@ typedef struct mdp_config {
     double gamma;                     /* --gamma (TD target in fp64, maddpg.py:186) */
     uint64_t seed;                    /* device Philox key (Gumbel noise, env resets) */
     int32_t episode_log_rows;         /* finished-episode log ring (0: max(4096, 4 num_envs));
+                                         otherwise >= 2 num_envs (mdp_create fails below);
                                          train.py sizes it save_rate + 2 num_envs */
     int32_t reserved;
 } mdp_config;
@@ -207,6 +208,13 @@ int mdp_dp_xgmi_close(mdp_handle* h);
  * 2 direct xGMI), ranks in the communicator (ncclCommCount / exchange world),
  * this rank, peers reached (RCCL: ranks - 1; xGMI: peer buffers mapped)} */
 int mdp_dp_info(mdp_handle* h, int32_t out4[4]);
+/* what the direct xGMI exchange cost this rank (in-kernel s_memrealtime stamps
+ * of k_reduce_apply's chunk workgroups: from a chunk's own stores to the
+ * arrival of every peer's copy -- peer skew plus fabric latency): out4 =
+ * {chunk exchanges counted, mean wait us, longest wait us, total wait us}
+ * since the last reset; reset != 0 zeroes the counters.  The RCCL path's cost
+ * is event-timed instead (mdp_prof_enable(MDP_K_ALLREDUCE)). */
+int mdp_dp_exchange_stats(mdp_handle* h, double out4[4], int32_t reset);
 /* Co-residency plan of the spin-waiting optimizer launch (k_reduce_apply: the
  * chunk workgroups of a tensor wait for each other's norm partials, the xGMI
  * exchange for the peers' chunks).  For cfg on a device with `cus` CUs that
@@ -234,7 +242,10 @@ int mdp_get_stats(mdp_handle* h, int32_t agent, double out6[6]);
  *   every clip + Adam + Polyak -- 3 launches per round.  With data parallelism
  *   (mdp_dp_init BEFORE this call): gradients, a reduce pass, ONE all-reduce
  *   of the whole gradient region per round, the step pass (x 1/world).  Needs
- *   the fast H=64 kernels (mdp_grad_variant == 1) for every agent. */
+ *   the fused optimizer step for every net (mdp_create's co-residency plan)
+ *   and <= 8 agents; the fast H=64 kernels batch every agent's gradients in
+ *   one launch, the general kernels (H=128/256, > 3 target actors) run one
+ *   gradient launch per agent and step kind. */
 int mdp_set_update_mode(mdp_handle* h, int32_t mode);
 /* one throughput-mode round with injected randomness (the parity entry point,
  * like mdp_update): idx_dev [n][B] (NULL: drawn from the index stream),
@@ -270,7 +281,8 @@ int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out_host);
 enum mdp_kernel_kind {
     MDP_K_INDEX = 0, MDP_K_GATHER = 1, MDP_K_CRITIC_GRAD = 2, MDP_K_ACTOR_GRAD = 3,
     MDP_K_APPLY = 4, MDP_K_ROLLOUT = 5, MDP_K_REDUCE = 6, MDP_K_REDUCE_APPLY = 7,
-    MDP_K_COUNT = 8
+    MDP_K_ALLREDUCE = 8,   /* the RCCL data-parallel all-reduces (not a kernel of this library) */
+    MDP_K_COUNT = 9
 };
 int mdp_prof_enable(mdp_handle* h, int32_t kind, int32_t on);
 /* which grad kernels serve `agent`: 1 = register-resident k_*_grad_r (H = 64

@@ -22,7 +22,7 @@ MAX_AGENTS = 8
 ACT_DIM = 5
 BENCH_W = 8   # MDP_BENCH_W: floats per agent benchmark_data record
 MAX_UNITS = 256  # MDP_MAX_UNITS: largest --num-units
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 SCN = {"none": 0, "simple": 1, "simple_spread": 2, "simple_adversary": 3, "simple_tag": 4}
 WHICH = {"actor": 0, "critic": 1, "tgt_actor": 2, "tgt_critic": 3, "m_actor": 4, "v_actor": 5,
@@ -30,7 +30,7 @@ WHICH = {"actor": 0, "critic": 1, "tgt_actor": 2, "tgt_critic": 3, "m_actor": 4,
 REGION = {"theta": 0, "target": 1, "adam_m": 2, "adam_v": 3, "grad": 4, "replay": 5, "index": 6,
           "stats": 7, "env": 8, "eplog": 9, "beta": 10, "slab": 11, "ctl": 12}
 KERNEL = {"index": 0, "gather": 1, "critic_grad": 2, "actor_grad": 3, "apply": 4, "rollout": 5,
-          "reduce": 6, "reduce_apply": 7}
+          "reduce": 6, "reduce_apply": 7, "allreduce": 8}
 
 
 class MdpConfig(ctypes.Structure):
@@ -117,6 +117,7 @@ SIGNATURES = {
     "mdp_dp_xgmi_enable": (ctypes.c_int, [_P]),
     "mdp_dp_xgmi_close": (ctypes.c_int, [_P]),
     "mdp_dp_info": (ctypes.c_int, [_P, _I32P]),
+    "mdp_dp_exchange_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), _I32]),
     "mdp_ra_plan": (ctypes.c_int, [ctypes.POINTER(MdpConfig), _I32, _I32, _I32P]),
     "mdp_critic_grad": (ctypes.c_int, [_P, _I32, _P, _P]),
     "mdp_actor_grad": (ctypes.c_int, [_P, _I32, _P, _P]),

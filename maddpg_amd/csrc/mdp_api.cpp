@@ -193,6 +193,13 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   }
   L.n_ent = n + L.env.n_landmarks;
   if (c->episode_log_rows < 0) { err = "episode_log_rows < 0"; return false; }
+  // lockstep logging writes slot ep_base + e for every env finishing in one
+  // step: a ring shorter than two steps' worth would overwrite records of the
+  // same or the previous step before a reader (LearningCurve) sees them
+  if (c->episode_log_rows > 0 && (int64_t)c->episode_log_rows < 2 * (int64_t)E) {
+    err = "episode_log_rows must be 0 (default) or at least 2 * num_envs";
+    return false;
+  }
   L.eplog_rows = c->episode_log_rows > 0 ? c->episode_log_rows : std::max(4096, 4 * E);
   int64_t sz[MDP_R_COUNT];
   sz[MDP_R_THETA] = sz[MDP_R_TARGET] = sz[MDP_R_ADAM_M] = sz[MDP_R_ADAM_V] = sz[MDP_R_GRAD] = 4 * L.PT;
@@ -207,8 +214,7 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   sz[MDP_R_SLAB] = (int64_t)n * (4 * (int64_t)L.nwg * (L.slab_c + L.slab_a) + 2 * 8 * 8 * (int64_t)L.nwg +
                                   8 * (int64_t)c->batch_size) + 256 + 256 + mdp_ra_sync_bytes() +
                    4 * (int64_t)L.nwg * 16 * (MDP_APRE_W + MDP_CPRE_W + 2 * T.row_stride) +  // precomputed work + rows
-                   4 * (int64_t)mdp_pair_rows(c->batch_size) * MDP_ACT_DIM * n + 8 * (int64_t)n * L.nwg +
-                   512;  // pair hand-off (whole pairs of rows) + counters
+                   512;  // counters
   sz[MDP_R_CTL] = sizeof(Ctl);
   int64_t o = 0;
   for (int r = 0; r < MDP_R_COUNT; ++r) {
@@ -300,16 +306,6 @@ struct mdp_handle {
   bool critic_pre = true;
   float* apre_rows = nullptr;  // the replay rows those launches gathered (read contiguously by the step)
   float* cpre_rows = nullptr;
-  // general critic step as pairs of workgroups per 32 rows (mdp_grads_pair.hip),
-  // opt-in with MDP_PAIR=1 (measured slower than k_critic_grad at S5: DESIGN §4)
-  bool pair_mode = false;
-  // general critic step: the target actions by a k_target_act launch in front
-  // of k_critic_grad (MADDPG critics), opt-in with MDP_TARGET_ACT=1 (measured
-  // slower at S5: DESIGN §4); default: inside the critic kernel
-  bool target_act = false;
-  float* pair_xa = nullptr;  // [B][5 n] a~ of the pair kernel and of k_target_act
-  uint32_t* pair_prod = nullptr;
-  uint32_t* pair_cons = nullptr;
   hipGraph_t round_graph = nullptr;
   hipGraphExec_t round_exec = nullptr;
   // mdp_train_step graphs (rollout + k rounds), one per k
@@ -459,31 +455,6 @@ int launch_make_index(mdp_handle* h, int count, int32_t* out) {
 
 bool tp_fast(const mdp_handle* h);
 
-// which critic kernel serves agent `agent`: the fast register-resident one
-// (strict order, H = 64 topologies), else the general one -- as the pair kernel
-// (MADDPG critics, H <= 128, its LDS fits) with MDP_PAIR=1
-bool crit_general(const mdp_handle* h, int agent, bool tp) {
-  return tp ? !tp_fast(h) : (h->general_grads || !grads_r_ok(h->L.topo, agent));
-}
-// target actors per pass of the pair kernel's actor workgroup: the fewest
-// passes the LDS budget allows, the actors spread evenly over them (0: none fit)
-int pair_group(const Topo& T) {
-  int G = T.n;
-  while (G > 0 && lds_pair_bytes(T, G) > MDP_LDS_BUDGET) --G;
-  if (G == 0) return 0;
-  const int passes = (T.n + G - 1) / G;
-  return (T.n + passes - 1) / passes;
-}
-bool pair_ok(const mdp_handle* h, int agent, bool tp) {
-  const Topo& T = h->L.topo;
-  return h->pair_mode && crit_general(h, agent, tp) && !T.ag[agent].local_q && (T.H == 64 || T.H == 128) &&
-         pair_group(T) > 0;
-}
-// partial-gradient slabs the critic step of `agent` leaves: one per 16 rows,
-// one per 32 with the pair kernel
-int crit_nwg(const mdp_handle* h, int agent, bool tp) {
-  return pair_ok(h, agent, tp) ? (h->cfg.batch_size + MDP_PAIR_R - 1) / MDP_PAIR_R : h->L.nwg;
-}
 
 // tp: throughput mode on the general kernels -- this agent's own blocks of
 // partials / stats / TD targets and noise counter upd_ctr + agent (multi = 2
@@ -497,9 +468,6 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.cpre_rows = h->cpre_rows;
   a.apre_rows = h->apre_rows;
   a.cpre_prev = post_prev;
-  a.pair_xa = nullptr;
-  a.pair_prod = a.pair_cons = nullptr;
-  a.xa = nullptr;
   a.multi = tp ? 2 : 0;
   a.slab_agent_stride = 0;
   a.pf_ctl = h->ctl;
@@ -535,26 +503,6 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
     if (apre) a.apre = h->apre;
     if (post_prev >= 0) a.cpre = h->cpre;
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
-    return 0;
-  }
-  if (pair_ok(h, agent, tp)) {
-    const Topo& T = h->L.topo;
-    a.group = pair_group(T);
-    a.pair_xa = h->pair_xa;
-    a.pair_prod = h->pair_prod + (int64_t)agent * h->L.nwg;
-    a.pair_cons = h->pair_cons + (int64_t)agent * h->L.nwg;
-    HIPCHK(h, mdp_launch_critic_pair(a, T.H, lds_pair_bytes(T, a.group), h->stream));
-    return 0;
-  }
-  if (h->target_act && !h->L.topo.ag[agent].local_q) {  // a~ by its own launch, then the critic step
-    // one actor slot pair stays allocated: the target critic and the backward
-    // use activation slot 0 as scratch while the critic's h1 / h2 (slot G) live on
-    a.xa = h->pair_xa;
-    a.group = 1;
-    if (lds_critic_bytes(h->L.topo, 1) > MDP_LDS_BUDGET || lds_target_act_bytes(h->L.topo) > MDP_LDS_BUDGET)
-      return fail(h, "critic step does not fit in LDS");
-    HIPCHK(h, mdp_launch_target_act(a, h->L.topo.H, h->stream));
-    HIPCHK(h, mdp_launch_critic_grad(a, h->L.topo.H, lds_critic_bytes(h->L.topo, 1), h->stream));
     return 0;
   }
   // as many target actors per pass as the LDS budget allows (all of them for S1-S4)
@@ -631,7 +579,7 @@ ApplyArgs apply_args(mdp_handle* h, int agent, int net, float scale, bool tp = f
   chunks(a.other, a.oblk);
   a.slab = nullptr;
   a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
-  a.nwg = net ? crit_nwg(h, agent, tp) : h->L.nwg;
+  a.nwg = h->L.nwg;
   a.scale = scale;
   a.clip = h->cfg.grad_clip;
   a.lr = h->cfg.lr;
@@ -735,7 +683,7 @@ int do_reduce(mdp_handle* h, int agent, int net) {
   const NDesc& d = net_of(h, agent, net);
   ReduceArgs a;
   a.slab = net ? h->slab_c : h->slab_a;
-  a.nwg = net ? crit_nwg(h, agent, false) : h->L.nwg;
+  a.nwg = h->L.nwg;
   a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
   a.grad = h->grad;
   a.off = d.off;
@@ -783,6 +731,7 @@ RcclApi& rccl() {
 int dp_allreduce(mdp_handle* h, int agent, int net) {
   const NDesc& d = net_of(h, agent, net);
   float* g = h->grad + d.off;
+  ProfScope p(h, MDP_K_ALLREDUCE);
   const ncclResult_t r = rccl().all_reduce(g, g, (size_t)d.size, ncclFloat32, ncclSum, h->comm, h->stream);
   if (r != ncclSuccess) {
     h->err = std::string("ncclAllReduce: ") + rccl().err(r);
@@ -793,6 +742,7 @@ int dp_allreduce(mdp_handle* h, int agent, int net) {
 
 // throughput mode: the whole grad region (every agent's actor + critic) in one call
 int dp_allreduce_all(mdp_handle* h) {
+  ProfScope p(h, MDP_K_ALLREDUCE);
   const ncclResult_t r = rccl().all_reduce(h->grad, h->grad, (size_t)h->L.PT, ncclFloat32, ncclSum, h->comm, h->stream);
   if (r != ncclSuccess) {
     h->err = std::string("ncclAllReduce: ") + rccl().err(r);
@@ -810,10 +760,14 @@ bool actor_pre_ok(const mdp_handle* h, int agent) {
 
 // agent k's critic step split around agent p's update (critic_pre in p's actor
 // launch, critic_post for k): fast kernels for both, k's critic MADDPG-style
-// (a DDPG critic needs no target actor but its own)
+// (a DDPG critic needs no target actor but its own).  p != k: the pre part
+// accumulates k's TARGET critic layer 1, which p's actor optimizer launch
+// Polyak-updates -- with k == p (one agent, carried across rounds) that
+// accumulator would be one Polyak step stale.
 bool critic_pre_ok(const mdp_handle* h, int p, int k) {
   const Topo& T = h->L.topo;
-  return h->critic_pre && !h->general_grads && grads_r_ok(T, p) && grads_r_ok(T, k) && !T.ag[k].local_q;
+  return p != k && h->critic_pre && !h->general_grads && grads_r_ok(T, p) && grads_r_ok(T, k) &&
+         !T.ag[k].local_q;
 }
 
 // strict data-parallel update of one agent (maddpg.py:188-194 order):
@@ -969,9 +923,6 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
     a.cpre = nullptr;
     a.cpre_rows = nullptr;
     a.cpre_prev = -1;
-    a.pair_xa = nullptr;
-    a.pair_prod = a.pair_cons = nullptr;
-    a.xa = nullptr;
     a.pf_ctl = h->ctl;
     a.pf_out = pf_out;
     a.pf_count = pf_out ? n * h->cfg.batch_size : 0;
@@ -1138,10 +1089,6 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->actor_pre = !(ap && ap[0] == '0');
     const char* cp = getenv("MDP_CRITIC_PRE");
     h->critic_pre = !(cp && cp[0] == '0');
-    const char* pm = getenv("MDP_PAIR");
-    h->pair_mode = pm && pm[0] == '1';
-    const char* ta = getenv("MDP_TARGET_ACT");
-    h->target_act = ta && ta[0] == '1';
   }
   if (!arena_dev || arena_bytes < h->L.total) {
     h->err = "arena missing or too small";
@@ -1212,10 +1159,6 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->cpre = h->apre + (int64_t)nwg * 16 * MDP_APRE_W;
     h->apre_rows = h->cpre + (int64_t)nwg * 16 * MDP_CPRE_W;
     h->cpre_rows = h->apre_rows + (int64_t)nwg * 16 * h->L.topo.row_stride;
-    h->pair_xa = h->cpre_rows + (int64_t)nwg * 16 * h->L.topo.row_stride;
-    h->pair_prod = (uint32_t*)(((uintptr_t)(h->pair_xa + mdp_pair_rows(cfg->batch_size) * MDP_ACT_DIM * na) + 255) &
-                               ~uintptr_t(255));
-    h->pair_cons = h->pair_prod + na * nwg;
   }
   HIPCHK(h, hipMemsetAsync(h->arena, 0, h->L.total, h->stream));
   std::vector<float> beta(8 * cfg->n_agents);
@@ -1744,6 +1687,23 @@ int mdp_dp_info(mdp_handle* h, int32_t out4[4]) {
     if (rccl().count && rccl().count(h->comm, &c) != ncclSuccess) return fail(h, "ncclCommCount failed");
     out4[1] = c;
     out4[3] = c - 1;
+  }
+  return 0;
+}
+
+int mdp_dp_exchange_stats(mdp_handle* h, double out4[4], int32_t reset) {
+  if (!h || !out4) return -1;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  uint64_t w[3] = {0, 0, 0};
+  HIPCHK(h, hipMemcpy(w, &h->ctl->xw_ticks, sizeof(w), hipMemcpyDeviceToHost));
+  const double us_per_tick = 0.01;  // s_memrealtime: 100 MHz
+  out4[0] = (double)w[1];
+  out4[1] = w[1] ? (double)w[0] * us_per_tick / (double)w[1] : 0.0;
+  out4[2] = (double)w[2] * us_per_tick;
+  out4[3] = (double)w[0] * us_per_tick;
+  if (reset) {
+    HIPCHK(h, hipMemsetAsync(&h->ctl->xw_ticks, 0, sizeof(w), h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
   }
   return 0;
 }

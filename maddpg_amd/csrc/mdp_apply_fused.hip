@@ -70,8 +70,10 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
+// wstat (optional): Ctl::xw_ticks -- lane 0 adds this chunk's wait (ticks
+// from its stores to the last peer word's arrival), the count and the maximum
 __device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc* xdp, uint32_t* fault, f32x4 g, int64_t i0, bool act,
-                                           uint32_t ep) {
+                                           uint32_t ep, uint64_t* wstat = nullptr) {
   const int W = __builtin_amdgcn_readfirstlane(xdp->world), r = __builtin_amdgcn_readfirstlane(xdp->rank);
   const int64_t pt = (int64_t)uni64((uint64_t)xdp->pt);
   uint64_t base[MDP_XCH_MAXW];
@@ -94,7 +96,7 @@ __device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc* xdp, uint32_t* fault
   // every peer's 4 words in flight at once (one round trip for the whole
   // world, not one per peer), re-read together until all carry this epoch
   float pv[MDP_XCH_MAXW][4];
-  uint64_t t0 = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (true) {
     uint64_t w[MDP_XCH_MAXW][4];
 #pragma unroll
@@ -118,11 +120,16 @@ __device__ __forceinline__ f32x4 xchg_chunk(const XchgDesc* xdp, uint32_t* fault
     }
     if (all || gone) break;
     __builtin_amdgcn_s_sleep(1);
-    if (t0 == 0) t0 = __builtin_amdgcn_s_memrealtime();
     if (__builtin_amdgcn_s_memrealtime() - t0 > kXchgTimeoutTicks) {
       __hip_atomic_store(fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
+  }
+  if (wstat && act && (threadIdx.x & 63) == 0) {
+    const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+    __hip_atomic_fetch_add(wstat, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(wstat + 1, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(wstat + 2, dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // the world's sum in rank order (identical on every rank)
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
@@ -237,7 +244,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
 #pragma unroll
       for (int q = 1; q < 16; ++q) g += red[q][col];
       MDP_STAMP(34);
-      if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ctr_use(ep_raw) + 1u);
+      if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ctr_use(ep_raw) + 1u, &a.ctl->xw_ticks);
       double ss = 0.0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {

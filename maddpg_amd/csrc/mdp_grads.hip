@@ -519,13 +519,6 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     copy_cols16(rowbuf, ldr, ag.act_off, xl, ldc, ag.obs_dim, MDP_ACT_DIM);
   } else {
     copy_cols16(rowbuf, ldr, T.ag[0].nobs_off, xt, ldc, 0, T.sum_obs);
-    if (a.xa) {  // the target actions of k_target_act (rows past the batch: zeros)
-      const int na5 = MDP_ACT_DIM * T.n;
-      for (int e = tid; e < MDP_R * na5; e += blockDim.x) {
-        const int row = e / na5, c = e - row * na5;
-        xt[row * ldc + T.sum_obs + c] = row < nvalid ? a.xa[(int64_t)(r0 + row) * na5 + c] : 0.f;
-      }
-    }
   }
   if (tid < MDP_MAX_AGENTS + 4) cnt[tid] = 0;
   __syncthreads();
@@ -535,11 +528,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
 
   // target actors of the group (+ the critic forward with the first group): each
   // layer phase deals every net's 16-column tiles over all waves
-  // with a.xa the target actions are in xt already: one pass with the critic
-  // forward (and the target critic's obs' part) only; G = 1 all the same (slot 0
-  // is the target critic's and the backward's scratch)
-  const int nact = a.xa ? 0 : (lq ? 1 : T.n);
-  const int npass = a.xa ? 1 : (nact + G - 1) / G;
+  const int nact = lq ? 1 : T.n;
+  const int npass = (nact + G - 1) / G;
   // the target critic's obs' part of layer 1 (maddpg.py:86) does not depend on
   // the target actions: with the first layer-1 phase, raw, into xl (unused by a
   // MADDPG critic); only the a~ rows remain after the Gumbel sample
@@ -984,129 +974,8 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   MDP_STAMP(60);
 }
 
-// ------------------------------------------------- target actions (S5 critic)
-// k_target_act: a~_j = gumbel_softmax(target_actor_j(obs'_j)) of the critic
-// step's batch for every agent j (maddpg.py:183-184), as a launch of its own in
-// front of k_critic_grad (CriticArgs::xa).  In the critic kernel each of the
-// 16-row workgroups streamed all n target actors' weights (476 KB of its 830 KB
-// at tag N=6, H=128) for 16 rows -- 8 flops per weight byte, co-bound with the
-// per-CU weight stream.  Here a 4-wave workgroup owns one actor and 64 rows
-// (32 at H = 256): a wave holds RTW row tiles x one 64-column group, so each
-// 16-byte weight load feeds 4 RTW MFMAs.  Every output is the same MFMA k-chain
-// (k ascending from a zero accumulator, steps past K skipped), the same bias /
-// ReLU, head and Gumbel-softmax operations as the in-kernel path, so a~ is
-// bit-identical to it (test_target_act_launch_bit_identical).
-template <int H>
-struct TaShape {
-  static constexpr int NG = H / 64;                  // 64-column groups
-  static constexpr int RTW = H == 64 ? 1 : 2;        // row tiles per wave
-  static constexpr int RT = (4 / NG) * RTW;          // row tiles per workgroup
-  static constexpr int ROWS = 16 * RT;
-};
-
-namespace {
-// Y[rows of tiles rt0 .. rt0 + RTW - 1][64 g .. 64 g + 63] = relu(X W + b) on one wave
-template <int RTW>
-__device__ __forceinline__ void ta_layer(const float* X, int ldx, int K, const float* __restrict__ W,
-                                         const float* __restrict__ b, int N, float* Y, int ldy, int g, int rt0) {
-  constexpr int KS = MDP_GKS;
-  const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4, col4 = 64 * g + 4 * r;
-  f32x4 acc[RTW][4];
-#pragma unroll
-  for (int q = 0; q < RTW; ++q)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[q][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const f32x4 bias = *reinterpret_cast<const f32x4*>(b + col4);
-  auto step = [&](const f32x4(&w)[KS], int c0) {
-#pragma unroll
-    for (int q = 0; q < RTW; ++q) rg_acc<KS>(acc[q], X + (rt0 + q) * 16 * ldx, ldx, r, c0, K, kq, w);
-  };
-  f32x4 wa[KS], wb[KS];
-  rg_load<KS>(wa, W, N, col4, 0, K, kq);
-  for (int c0 = 0; c0 < K; c0 += 8 * KS) {
-    const bool hb = c0 + 4 * KS < K;
-    if (hb) rg_load<KS>(wb, W, N, col4, c0 + 4 * KS, K, kq);
-    step(wa, c0);
-    if (!hb) break;
-    if (c0 + 8 * KS < K) rg_load<KS>(wa, W, N, col4, c0 + 8 * KS, K, kq);
-    step(wb, c0 + 4 * KS);
-  }
-#pragma unroll
-  for (int q = 0; q < RTW; ++q) {
-    float* Yq = Y + (rt0 + q) * 16 * ldy + col4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) Yq[(kq * 4 + i) * ldy + t] = fmaxf(acc[q][t][i] + bias[t], 0.f);
-  }
-}
-}  // namespace
-
-// grid (ceil(B / ROWS), n actors), 256 threads; xa[B][5 n]: a~_j at columns 5 j ..
-template <int H>
-__global__ __launch_bounds__(256) void k_target_act(CriticArgs a) {
-  using S = TaShape<H>;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Topo& T = a.topo;
-  const int j = blockIdx.y;
-  const ADesc& aj = T.ag[j];
-  const NDesc& an = aj.actor;
-  const float* P = a.target;
-  const int ldo = lds_ld(T.obs_max), ldh = H + 1;
-  LdsCarve cv(lds);
-  float* X = cv.take(S::ROWS * ldo);
-  float* H1 = cv.take(S::ROWS * ldh);
-  float* H2 = cv.take(S::ROWS * ldh);
-  float* LG = cv.take(S::ROWS * 8);
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r0 = blockIdx.x * S::ROWS;
-  const int nvalid = min(S::ROWS, a.B - r0);
-  const uint32_t ctr = a.ctl->upd_ctr + (a.multi > 1 ? (uint32_t)a.agent : 0u);
-  // the head's fragments first (one round trip, hidden behind the gather and layers)
-  float hw[H / 4], hbias;
-  head_load<H / 4>(hw, hbias, P + an.t[4].off, P + an.t[5].off, MDP_ACT_DIM);
-  // obs'_j of the rows (rows past the batch: zeros, as gather_rows16)
-  for (int e = tid; e < S::ROWS * aj.obs_dim; e += 256) {
-    const int row = e / aj.obs_dim, c = e - row * aj.obs_dim;
-    X[row * ldo + c] = row < nvalid ? a.replay[(int64_t)a.idx[r0 + row] * T.row_stride + aj.nobs_off + c] : 0.f;
-  }
-  __syncthreads();
-  const int g = wave % S::NG, rt0 = (wave / S::NG) * S::RTW;
-  ta_layer<S::RTW>(X, ldo, aj.obs_dim, P + an.t[0].off, P + an.t[1].off, H, H1, ldh, g, rt0);
-  __syncthreads();
-  ta_layer<S::RTW>(H1, ldh, H, P + an.t[2].off, P + an.t[3].off, H, H2, ldh, g, rt0);
-  __syncthreads();
-  for (int rt = wave; rt < S::RT; rt += 4) head_acc<H / 4>(hw, hbias, H2 + rt * 16 * ldh, ldh, MDP_ACT_DIM, LG + rt * 16 * 8, 8);
-  __syncthreads();
-  if (tid < nvalid) {  // distributions.py:264-266, the in-kernel path's noise stream
-    const int row = r0 + tid;
-    float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
-    if (a.u_tgt) {
-      for (int k = 0; k < MDP_ACT_DIM; ++k) u[k] = a.u_tgt[((int64_t)j * a.B + row) * MDP_ACT_DIM + k];
-    } else {
-      uniforms5(a.seed, (uint32_t)((a.agent << 8) | (j + 1)), ctr, (uint32_t)row, u);
-    }
-    gumbel_softmax5(LG + tid * 8, u, act);
-    float* dst = a.xa + (int64_t)row * (MDP_ACT_DIM * T.n) + MDP_ACT_DIM * j;
-    for (int k = 0; k < MDP_ACT_DIM; ++k) dst[k] = act[k];
-  }
-}
-
 // ---------------------------------------------------------------- launchers
 namespace {
-template <int H>
-hipError_t launch_target_act(const CriticArgs& a, int lds, hipStream_t s) {
-  using S = TaShape<H>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_target_act<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              MDP_LDS_BUDGET);
-    (void)hipGetLastError();
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_target_act<H>, dim3((a.B + S::ROWS - 1) / S::ROWS, a.topo.n), dim3(256), lds, s, a);
-  return hipGetLastError();
-}
 template <int H>
 hipError_t launch_critic(const CriticArgs& a, int lds, hipStream_t s) {
   static bool attr = false;
@@ -1138,14 +1007,6 @@ hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hip
     case 64: return launch_critic<64>(a, lds_bytes, s);
     case 128: return launch_critic<128>(a, lds_bytes, s);
     case 256: return launch_critic<256>(a, lds_bytes, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-hipError_t mdp_launch_target_act(const CriticArgs& a, int H, hipStream_t s) {
-  switch (H) {
-    case 64: return launch_target_act<64>(a, lds_target_act_bytes(a.topo), s);
-    case 128: return launch_target_act<128>(a, lds_target_act_bytes(a.topo), s);
-    case 256: return launch_target_act<256>(a, lds_target_act_bytes(a.topo), s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -50,17 +50,6 @@ struct CriticArgs {
   const float* cpre;
   const float* cpre_rows;  // the replay rows the critic_pre gathered, [B][row_stride]
   int cpre_prev;
-  // k_critic_pair (general kernels, MADDPG critics): per 32 batch rows a pair
-  // of workgroups -- the target actors' workgroup hands the target actions a~
-  // over through pair_xa [B][5 n] and bumps pair_prod[p]; the critic's
-  // workgroup waits until pair_prod[p] passes its own count pair_cons[p]
-  float* pair_xa;
-  uint32_t* pair_prod;
-  uint32_t* pair_cons;
-  // general critic step (k_critic_grad): the target actions a~ [B][5 n] of
-  // every agent, computed by a k_target_act launch in front of it (k_target_act
-  // writes them here); null: the critic kernel runs the target actors itself
-  float* xa;
   Topo topo;
 };
 
@@ -274,29 +263,6 @@ inline int lds_actor_bytes(const Topo& t) {
   return 4 * (mdp_r4(R * ldr) + mdp_r4(R * ldc) + 6 * mdp_r4(S) + 5 * mdp_r4(R * 8) + mdp_r4(5 * t.H));
 }
 #define MDP_LDS_BUDGET (160 * 1024)
-// k_target_act (mdp_grads.hip): obs' rows, h1, h2, logits of 64 rows (32 at H = 256)
-inline int lds_target_act_bytes(const Topo& t) {
-  const int R = t.H == 256 ? 32 : 64, ldo = mdp_ld(t.obs_max), ldh = t.H + 1;
-  return 4 * (mdp_r4(R * ldo) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8));
-}
-// paired general critic step (mdp_grads_pair.hip): 32 rows per pair; the
-// target-actor workgroup holds obs' and G actors' h1/h2/logits, the critic
-// workgroup the rows, h1/h2 of the critic, the target critic's obs' partial,
-// its h1/h2 (then the deltas) and the target actions
-#define MDP_PAIR_R 32
-inline int64_t mdp_pair_rows(int64_t B) { return (B + MDP_PAIR_R - 1) / MDP_PAIR_R * MDP_PAIR_R; }
-inline int lds_pair_a_bytes(const Topo& t, int G) {
-  const int R = MDP_PAIR_R, ldo = mdp_ld(t.sum_obs + 4), S = R * (t.H + 1);
-  return 4 * (mdp_r4(R * ldo) + 2 * G * mdp_r4(S) + mdp_r4(G * R * 8));
-}
-inline int lds_pair_b_bytes(const Topo& t) {
-  const int R = MDP_PAIR_R, ldr = mdp_ld(t.row_stride), S = R * (t.H + 1), ldx = mdp_ld(5 * t.n);
-  return 4 * (mdp_r4(R * ldr) + 5 * mdp_r4(S) + mdp_r4(R * ldx) + 3 * mdp_r4(R * 8) + mdp_r4(R));
-}
-inline int lds_pair_bytes(const Topo& t, int G) {
-  const int a = lds_pair_a_bytes(t, G), b = lds_pair_b_bytes(t);
-  return a > b ? a : b;
-}
 // fast (register-resident, H = 64) variants in mdp_grads_r.hip
 inline int lds_critic_r_bytes(const Topo& t, int agent) {
   const int R = 16, ldr = mdp_ld(t.row_stride), LH = 68, LD = 65;
@@ -336,10 +302,6 @@ inline int lds_eval_bytes(int in, int H) {
 }
 
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
-// paired general critic step: grid 2 ceil(B / 32), a.group target actors per pass
-hipError_t mdp_launch_critic_pair(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
-// the target actions of a general critic step into a.xa: grid (ceil(B / 64), n)
-hipError_t mdp_launch_target_act(const CriticArgs& a, int H, hipStream_t s);
 hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s);

@@ -62,4 +62,10 @@ struct Ctl {
   uint32_t xstep[16];   // xGMI exchanges completed per net (2 * agent + net): the epoch counter
   uint32_t ep_pending;  // episodes finished in the running rollout (the last workgroup folds it in)
   uint32_t pad1;
+  // xGMI exchange diagnostics (mdp_dp_exchange_stats): per chunk workgroup,
+  // the s_memrealtime ticks (100 MHz) from its own chunk's stores to the
+  // arrival of every peer's chunk -- peer skew + fabric latency
+  uint64_t xw_ticks;    // summed over chunk exchanges
+  uint64_t xw_count;    // chunk exchanges counted
+  uint64_t xw_max;      // the longest single wait
 };

@@ -441,6 +441,14 @@ class Engine:
         self._c("mdp_dp_info", out)
         return {"kind": self.DP_KINDS[out[0]], "ranks": out[1], "rank": out[2], "peers": out[3]}
 
+    def dp_exchange_stats(self, reset=False):
+        """direct xGMI exchange wait of this rank's chunk workgroups since the
+        last reset (mdp_dp_exchange_stats): {chunk_exchanges, mean_us, max_us,
+        total_us}."""
+        out = (ctypes.c_double * 4)()
+        self._c("mdp_dp_exchange_stats", out, 1 if reset else 0)
+        return {"chunk_exchanges": int(out[0]), "mean_us": out[1], "max_us": out[2], "total_us": out[3]}
+
     def param_checksum(self):
         """exact fingerprint of every replicated state region (weights, targets,
         Adam moments, beta powers): int64 sums of the raw 32-bit words, plus a

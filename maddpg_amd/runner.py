@@ -22,6 +22,24 @@ def rounds_due(t_before, t_after, every=100):
     return t_after // every - t_before // every
 
 
+def select_exchange(eng, world_size, rank, environ=None):
+    """Which gradient exchange a data-parallel rank runs over, decided the
+    same on every rank: the direct xGMI exchange when every rank opened,
+    connected and probed it (parallel.xgmi_handshake; a peer that never
+    answers the probe fails it after the probe's bounded wait), else the
+    library's own RCCL communicator, else torch.distributed (strict_round).
+    Returns (native_dp, kind)."""
+    env = os.environ if environ is None else environ
+    if world_size <= 1:
+        return False, None
+    if env.get("MDP_NATIVE_DP", "1") == "1":
+        if env.get("MDP_DP_XGMI", "1") == "1" and eng.dp_xgmi_init_from_dist(world_size, rank):
+            return True, "native-xgmi"
+        if eng.dp_init_from_dist(world_size, rank):
+            return True, "native-rccl"
+    return False, "torch.distributed"
+
+
 class VecRunner:
     def __init__(self, scenario="simple_spread", num_envs=1024, *, n_agents=None, scenario_adversaries=None,
                  num_adversaries=0, good_policy="maddpg", adv_policy="maddpg", batch_size=1024,
@@ -55,16 +73,7 @@ class VecRunner:
         # MDP_NATIVE_DP=0 keeps the torch.distributed path (strict_round).  The
         # exchange is the direct xGMI one inside the optimizer kernel when every
         # rank can map every peer (MDP_DP_XGMI=0: RCCL all-reduces instead)
-        self.native_dp = False
-        self.dp_kind = None
-        if world_size > 1 and os.environ.get("MDP_NATIVE_DP", "1") == "1":
-            if os.environ.get("MDP_DP_XGMI", "1") == "1" and self.eng.dp_xgmi_init_from_dist(world_size, rank):
-                self.native_dp, self.dp_kind = True, "native-xgmi"
-            else:
-                self.native_dp = self.eng.dp_init_from_dist(world_size, rank)
-                self.dp_kind = "native-rccl" if self.native_dp else None
-        if world_size > 1 and self.dp_kind is None:
-            self.dp_kind = "torch.distributed"
+        self.native_dp, self.dp_kind = select_exchange(self.eng, world_size, rank)
 
     def rollout(self):
         self.eng.env_step()

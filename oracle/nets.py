@@ -87,9 +87,29 @@ def softmax_bwd(a, da):
     return ((da - (da * a).sum(-1, keepdims=True)) * a).astype(F32)
 
 
-def clip_by_norm(g, c=0.5):
+# How clip_by_norm takes the tensor norm.  "fp64" (default): the sum of
+# squares in float64, rounded to fp32 after the sqrt -- the value every fp32
+# summation order approximates, and what the device optimizer computes (fp64
+# per-chunk sums, combined in chunk order).  "fp32": TF1's own arithmetic
+# (clip_ops.clip_by_norm: l2norm = sqrt(reduce_sum(t * t)) with t * t and the
+# sum in fp32; numpy's pairwise order stands in for Eigen's, which no
+# restatement reproduces bit for bit).  tests/test_gpu_parity.py reports the
+# device's distance to both.
+CLIP_NORM = "fp64"
+
+
+def tensor_norm(g, mode=None):
+    mode = mode or CLIP_NORM
+    if mode == "fp32":
+        g32 = g.astype(F32)
+        return np.sqrt(np.sum(g32 * g32, dtype=F32)).astype(F32)
+    return np.sqrt(np.sum(g.astype(np.float64) ** 2)).astype(F32)
+
+
+def clip_by_norm(g, c=0.5, mode=None):
+    """tf_util.py:178-180: (g * c) / max(||g||, c), per tensor."""
     c = F32(c)
-    n = np.sqrt(np.sum(g.astype(np.float64) ** 2)).astype(F32)
+    n = tensor_norm(g, mode)
     return ((g * c) / np.maximum(n, c)).astype(F32)
 
 

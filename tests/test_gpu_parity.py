@@ -151,6 +151,27 @@ def _device_grads(eng, agent, net):
     return out
 
 
+def _clip_mode_distance(eng, c, i, dgs):
+    """SURVEY App. A / tf_util.py:178-180: which clip_by_norm arithmetic the
+    device implements.  Agent i's first Adam step (from the case's pre-update
+    weights) re-run on the DEVICE's batch-reduced gradient with the tensor
+    norm taken in fp64 (the device's choice) and in fp32 (TF1's reduce_sum):
+    the worst |theta_device - theta_mode| per net and mode, and the worst
+    relative gap between the two norms over the net's tensors."""
+    out = {}
+    for net, w in ((1, "critic"), (0, "actor")):
+        dev = eng.get_params(i, w)
+        g = {k: np.asarray(v, np.float32).reshape(dev[k].shape) for k, v in dgs[net].items()}
+        n64 = {k: float(nets.tensor_norm(v, "fp64")) for k, v in g.items()}
+        n32 = {k: float(nets.tensor_norm(v, "fp32")) for k, v in g.items()}
+        out[(w, "norm_rel_gap")] = max(abs(n32[k] - n64[k]) / max(n64[k], 1e-30) for k in g)
+        for mode in ("fp64", "fp32"):
+            p = {k: np.asarray(v, np.float32).reshape(dev[k].shape).copy() for k, v in c["params"][i][w].items()}
+            nets.Adam(p).apply(p, {k: nets.clip_by_norm(v, 0.5, mode) for k, v in g.items()})
+            out[(w, mode)] = max(float(np.abs(dev[k] - p[k]).max()) for k in p)
+    return out
+
+
 def _update_parity(dims, B, L, seed, local_q=None, H=64, check_round=True):
     c = synthetic_trainer_case(dims, B, L, seed, local_q, H)
     n = len(dims)
@@ -160,15 +181,21 @@ def _update_parity(dims, B, L, seed, local_q=None, H=64, check_round=True):
         for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
             eng.set_params(i, w, p[w])
     agents = [trainer.AgentParams(**copy.deepcopy(p), local_q=c["local_q"][i]) for i, p in enumerate(c["params"])]
-    report, greport, wreport = [], [], []
+    report, greport, wreport, creport = [], [], [], []
     for i in range(n if check_round else 1):
         eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
                    u_act=torch.from_numpy(c["u_act"][i]))
         got = eng.stats(i)
         want, og = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i])
         conditioned = {}
+        dgs = {net: _device_grads(eng, i, net) for net in (0, 1)}
+        cm = _clip_mode_distance(eng, c, i, dgs)
+        creport.append(cm)
+        for w in ("critic", "actor"):
+            # the device's step IS the fp64-norm clip applied to its own gradient
+            assert cm[(w, "fp64")] < 1e-6, (i, w, cm)
         for net, name in ((1, "grad_critic"), (0, "grad_actor")):
-            dg = _device_grads(eng, i, net)
+            dg = dgs[net]
             for k, ref in og[name].items():
                 ref = np.asarray(ref, np.float64).reshape(dg[k].shape)
                 scale = float(np.abs(ref).max()) or 1.0
@@ -207,6 +234,11 @@ def _update_parity(dims, B, L, seed, local_q=None, H=64, check_round=True):
     print(f"   worst grad |diff|/max|g| = {max(r[3] for r in greport):.3e} (critic "
           f"{max(r[3] for r in greport if r[1] == 1):.3e}); worst conditioned param |diff| = "
           f"{max(r[3] for r in wreport):.3e}")
+    for w in ("critic", "actor"):
+        print(f"   clip_by_norm on the device gradient, {w}: theta vs fp64-norm step "
+              f"{max(r[(w, 'fp64')] for r in creport):.3e}, vs fp32-norm (TF1 reduce_sum) step "
+              f"{max(r[(w, 'fp32')] for r in creport):.3e}; |norm32 - norm64| / norm64 <= "
+              f"{max(r[(w, 'norm_rel_gap')] for r in creport):.3e}")
     return worst
 
 
@@ -247,29 +279,21 @@ def test_update_parity_tag4_h64_general_kernels():
     _update_parity([16, 16, 16, 14], B=512, L=2000, seed=26)
 
 
-@pytest.mark.parametrize("pair", ["1", "0"])
 @pytest.mark.parametrize("local_q", [None, [True, False, False]])
-def test_update_parity_general_kernels_forced(monkeypatch, local_q, pair):
-    # the general kernels (mdp_grads.hip) on a configuration the fast ones also
-    # serve; MADDPG critics on the pair kernel (mdp_grads_pair.hip) or, with
-    # MDP_PAIR=0, the single-workgroup one
+def test_update_parity_general_kernels_forced(monkeypatch, local_q):
+    # the general kernels (mdp_grads.hip) on a configuration the fast ones also serve
     monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
-    monkeypatch.setenv("MDP_PAIR", pair)
     _update_parity([18, 18, 18], B=256, L=1200, seed=27, local_q=local_q)
 
 
-def test_update_parity_pair_ragged_batch(monkeypatch):
-    # the pair kernel's last pair only partly filled (B = 200: 6 pairs + 8 rows)
+def test_update_parity_general_ragged_batch(monkeypatch):
+    # the general kernels' last 16-row tile only partly filled (B = 200: 12 tiles + 8 rows)
     monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
-    monkeypatch.setenv("MDP_PAIR", "1")
     _update_parity([18, 18, 18], B=200, L=900, seed=31)
 
 
-@pytest.mark.parametrize("pair", ["1", "0"])
-def test_update_parity_tag6_h128_ragged(monkeypatch, pair):
-    # tag N=6 at H=128, B = 1000: the pair kernel (31 pairs + 8 rows) and the
-    # single-workgroup kernel's work-queue layer phase (62 row tiles + 8 rows)
-    monkeypatch.setenv("MDP_PAIR", pair)
+def test_update_parity_tag6_h128_ragged():
+    # tag N=6 at H=128, B = 1000: the work-queue layer phase over 62 row tiles + 8 rows
     _update_parity([22, 22, 22, 22, 20, 20], B=1000, L=6000, seed=32, H=128)
 
 
@@ -623,20 +647,29 @@ def test_rollout_policy_actions_match_oracle():
         np.testing.assert_allclose(rows[:, lay[j]["act"]:lay[j]["act"] + ACT], want, atol=2e-6)
 
 
-@pytest.mark.parametrize("cap,general", [(20000, False), (3300, False), (20000, True)])
-def test_train_step_graph_equals_step_then_rounds(monkeypatch, cap, general):
+@pytest.mark.parametrize("scenario,adv_policy,cap,general", [
+    ("simple_spread", "maddpg", 20000, False),
+    ("simple_spread", "maddpg", 3300, False),
+    ("simple_spread", "maddpg", 20000, True),
+    ("simple", "maddpg", 20000, False),             # one agent: no critic split carried onto itself
+    ("simple_adversary", "ddpg", 20000, False),     # agent 0 a DDPG critic: the carry into it is skipped
+])
+def test_train_step_graph_equals_step_then_rounds(monkeypatch, scenario, adv_policy, cap, general):
     """mdp_train_step(k) (rollout + k rounds replayed as one graph; the first
     round's indices drawn by an extra rollout workgroup, the later rounds' by
     the fast critic kernel -- or, on the general kernels, in pieces by the
-    optimizer launches) is the same work as env_step + k x update_round:
-    bit-identical state and RNG stream after 4 steps.  cap=3300: the ring
-    fills during the steps (draws against the capped length)."""
+    optimizer launches; the critic split carried from a round's last actor
+    launch into the next round's agent 0) is the same work as env_step + k x
+    update_round (eager rounds, no carry): bit-identical state and RNG stream
+    after 4 steps.  cap=3300: the ring fills during the steps (draws against
+    the capped length)."""
     from maddpg_amd.runner import VecRunner
     if general:
         monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
 
     def make():
-        r = VecRunner("simple_spread", 64, batch_size=128, capacity=cap, seed=3, train_every=16)
+        r = VecRunner(scenario, 64, batch_size=128, capacity=cap, seed=3, train_every=16,
+                      num_adversaries=1 if scenario == "simple_adversary" else 0, adv_policy=adv_policy)
         r.prefill()
         return r
 
@@ -651,7 +684,7 @@ def test_train_step_graph_equals_step_then_rounds(monkeypatch, cap, general):
             b.train_round()
     a.eng.synchronize()
     b.eng.synchronize()
-    for i in range(3):
+    for i in range(a.n):
         for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
             pa, pb = a.eng.get_params(i, w), b.eng.get_params(i, w)
             for key in pa:
@@ -711,10 +744,13 @@ def test_env_benchmark_data_parity(name, n, na):
 def test_split_steps_bit_identical(monkeypatch, dims, local_q):
     """The actor step's forward computed in the critic launch (actor_pre) and
     the critic step split around the previous agent's update (critic_pre ->
-    critic_post, also across rounds of one training step) are scheduling
-    choices: the same MFMA chains in the same order.  Three rounds with both on
-    (update_round), with both off (MDP_ACTOR_PRE=0 MDP_CRITIC_PRE=0), and
-    agent by agent through mdp_update (no cross-agent split) must agree bit for bit."""
+    critic_post within a round) are scheduling choices: the same MFMA chains in
+    the same order.  Three rounds with both on (update_round), with both off
+    (MDP_ACTOR_PRE=0 MDP_CRITIC_PRE=0), and agent by agent through mdp_update
+    (no cross-agent split) must agree bit for bit.  The split carried ACROSS
+    rounds (mdp_train_step) is covered by
+    test_train_step_graph_equals_step_then_rounds, incl. one agent and a DDPG
+    agent 0."""
     B, L = 256, 3000
     c = synthetic_trainer_case(dims, B, L, seed=91, local_q=local_q)
     n = len(dims)
@@ -743,42 +779,4 @@ def test_split_steps_bit_identical(monkeypatch, dims, local_q):
             for k in a:
                 np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k} split vs unsplit")
                 np.testing.assert_array_equal(a[k], d[k], err_msg=f"{i} {w} {k} round vs per-agent")
-        np.testing.assert_array_equal(on.stats(i), off.stats(i))
-
-
-@pytest.mark.parametrize("dims,local_q,B,H,general", [
-    ([22, 22, 22, 22, 20, 20], None, 1000, 128, False),  # tag N=6 (S5 shape), ragged last tile
-    ([16, 16, 16, 14], None, 512, 64, False),            # 4 target actors at H = 64
-    ([8, 10, 10], [True, False, False], 256, 64, True),  # DDPG agent keeps the in-kernel actor
-    ([22, 22, 20], None, 96, 256, False),                 # H = 256: 32-row target-action tiles
-])
-def test_target_act_launch_bit_identical(monkeypatch, dims, local_q, B, H, general):
-    """The general critic step's target actions by a k_target_act launch of
-    their own (MDP_TARGET_ACT=1) or inside k_critic_grad (default): the same
-    MFMA k-chains, heads and Gumbel noise, so three update rounds agree bit for
-    bit -- parameters, Adam slots, targets and the six stats."""
-    L = 3000
-    c = synthetic_trainer_case(dims, B, L, seed=93, local_q=local_q, H=H)
-    n = len(dims)
-    if general:
-        monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
-
-    def run():
-        eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L)
-        eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
-        eng.init_params(5)
-        eng.seed_py_random(19)
-        for _ in range(3):
-            eng.update_round()
-        eng.synchronize()
-        return eng
-
-    off = run()
-    monkeypatch.setenv("MDP_TARGET_ACT", "1")
-    on = run()
-    for i in range(n):
-        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_critic", "v_critic"):
-            a, b = on.get_params(i, w), off.get_params(i, w)
-            for k in a:
-                np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k}")
         np.testing.assert_array_equal(on.stats(i), off.stats(i))
