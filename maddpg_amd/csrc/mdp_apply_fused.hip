@@ -458,15 +458,40 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
   }
 }
 
+// diagnostic build: every workgroup's start and end of the last launch (roles:
+// chunk workgroups, Polyak, stats, the draw piece last) -- which role ends it
+#ifdef MDP_STAMPS
+__device__ unsigned long long g_ra_t0[1024], g_ra_t1[1024];
+#define MDP_RA_WG(arr)                                                                 \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) arr[blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+extern "C" int mdp_debug_ra_wg(unsigned long long* t0, unsigned long long* t1, int n) {
+  if (hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_ra_t0), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(t1, HIP_SYMBOL(g_ra_t1), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#else
+#define MDP_RA_WG(arr) \
+  do {                 \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
+  MDP_RA_WG(g_ra_t0);
   MDP_KARG_TOUCH("s"(f.pf_count), "s"(f.xstep), "s"(f.ap.blk[0]), "s"(f.ap.target), "s"(f.ap.clip), "s"(f.ap.stats_mode),
                  "s"(f.ap.ctl), "s"(gridDim.x), "s"(f.ap.net.t[0].off), "s"(f.ap.net.t[4].cols), "s"(f.ap.other.t[2].off),
                  "s"(f.ap.other.in));
   if (f.pf_count > 0 && blockIdx.x == gridDim.x - 1) {  // a piece of the next round's index draw
     make_index_block<1024>(f.pf_ctl, f.pf_count, f.pf_out);
+    __syncthreads();
+    MDP_RA_WG(g_ra_t1);
     return;
   }
   reduce_apply_body(f, blockIdx.x, gridDim.x - (f.pf_count > 0 ? 1 : 0));
+#ifdef MDP_STAMPS
+  __syncthreads();
+  MDP_RA_WG(g_ra_t1);
+#endif
 }
 
 // throughput mode: the steps of several nets in one launch (each net's chunk
