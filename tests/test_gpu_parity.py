@@ -780,4 +780,3 @@ def test_split_steps_bit_identical(monkeypatch, dims, local_q):
                 np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k} split vs unsplit")
                 np.testing.assert_array_equal(a[k], d[k], err_msg=f"{i} {w} {k} round vs per-agent")
         np.testing.assert_array_equal(on.stats(i), off.stats(i))
-
