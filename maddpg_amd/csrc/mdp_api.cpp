@@ -878,6 +878,7 @@ int tp_setup(mdp_handle* h) {
   for (int ph = 0; ph < 4; ++ph) {
     RaBatch& rb = *rbs[ph];
     rb.count = 2 * n;
+    rb.narrow = h->L.nwg <= 64 ? 1 : 0;
     rb.wg_start[0] = 0;
     for (int i = 0; i < n; ++i)
       for (int net = 1; net >= 0; --net) {

@@ -171,10 +171,25 @@ hipError_t mdp_launch_xchg_probe(const XchgDesc* xd, uint32_t ep, int nchunk, ui
   return hipGetLastError();
 }
 
-// b: this workgroup's index among the nb workgroups of this net's step
+// ((r0 + r1) + (r2 + r3)) + ... over rows [LO, LO + N) of the group sums
+// (compile-time indices: a private array here stayed in scratch)
+template <int LO, int N>
+__device__ __forceinline__ f32x4 red_tree(const f32x4 (*red)[64], int col) {
+  if constexpr (N == 1)
+    return red[LO][col];
+  else
+    return red_tree<LO, N / 2>(red, col) + red_tree<LO + N / 2, N / 2>(red, col);
+}
+
+// b: this workgroup's index among the nb workgroups of this net's step;
+// G waves (G = 16: 1024-thread workgroups; G = 4: 256 threads, used exactly
+// when nwg <= 64 -- a launch of fewer waves dispatches sooner).  Wave q sums
+// partials w = q, q + G, ..., then a fixed tree over the waves: the summation
+// order is a function of nwg alone (every launch of a configuration agrees)
+template <int G>
 __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const int b, const uint32_t nb) {
   const ApplyArgs& a = f.ap;
-  __shared__ f32x4 red[16][64];
+  __shared__ f32x4 red[G][64];
   const int tid = threadIdx.x, lane = tid & 63;
   MDP_STAMP(30);
   if (f.phase == 1 && b >= f.rblk[6]) return;  // reduce-only pass: chunk workgroups only
@@ -210,25 +225,49 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       if (a.polyak) tg4 = ld4(a.target + i0);
     }
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    if (f.phase == 2) {  // step from the all-reduced gradient in grad[]
-      if (grp == 0 && act) s = ld4(a.grad + i0);
-    } else if (act) {
-      const float* base = a.slab + (td.off - a.net.off) + p0;
-      // partials w = grp + 16 k: up to 16 loads (B <= 4096) in flight at once,
-      // summed in the fixed order ((v0 + v1) + v2) + v3, then v4, v5, ...
-      f32x4 v[16];
+    if constexpr (G == 16) {
+      if (f.phase == 2) {  // step from the all-reduced gradient in grad[]
+        if (grp == 0 && act) s = ld4(a.grad + i0);
+      } else if (act) {
+        const float* base = a.slab + (td.off - a.net.off) + p0;
+        // partials w = grp + 16 k: up to 16 loads (B <= 4096) in flight at
+        // once, summed in the fixed order ((v0 + v1) + v2) + v3, then v4, v5, ...
+        f32x4 v[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int w = grp + 16 * k;
-        v[k] = w < a.nwg ? ld4(base + (int64_t)w * a.slab_stride) : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < 16; ++k) {
+          const int w = grp + 16 * k;
+          v[k] = w < a.nwg ? ld4(base + (int64_t)w * a.slab_stride) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        s = ((v[0] + v[1]) + v[2]) + v[3];
+#pragma unroll
+        for (int k = 4; k < 16; ++k)
+          if (grp + 16 * k < a.nwg) s += v[k];
+        for (int w = grp + 256; w < a.nwg; w += 16) s += ld4(base + (int64_t)w * a.slab_stride);
       }
-      s = ((v[0] + v[1]) + v[2]) + v[3];
+      red[grp][col] = s;
+    } else {
+      static_assert(G == 4, "narrow launch: 4 waves");
+      // nwg <= 64 (host-checked): wave grp sums partials w = grp + 4 k, all 16
+      // loads issued unconditionally (a partial past nwg re-reads the last one
+      // and is dropped by the select: a guarded load compiled to a branch per
+      // load), in the order ((v0 + v1) + v2) + v3, then v4, v5, ...
+      if (f.phase == 2) {
+        if (grp == 0 && act) s = ld4(a.grad + i0);
+      } else if (act) {
+        const float* base = a.slab + (td.off - a.net.off) + p0;
+        f32x4 v[16];
 #pragma unroll
-      for (int k = 4; k < 16; ++k)
-        if (grp + 16 * k < a.nwg) s += v[k];
-      for (int w = grp + 256; w < a.nwg; w += 16) s += ld4(base + (int64_t)w * a.slab_stride);
+        for (int k = 0; k < 16; ++k) v[k] = ld4(base + (int64_t)min(grp + 4 * k, a.nwg - 1) * a.slab_stride);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (grp + 4 * k >= a.nwg) v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        s = ((v[0] + v[1]) + v[2]) + v[3];
+#pragma unroll
+        for (int k = 4; k < 16; ++k)
+          if (grp + 4 * k < a.nwg) s += v[k];
+      }
+      red[grp][col] = s;
     }
-    red[grp][col] = s;
     __syncthreads();
     MDP_STAMP(31);
     if (grp == 0 && f.phase != 1 && a.stats_mode) {
@@ -240,9 +279,9 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       if (lane == 0) __hip_atomic_fetch_add(f.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (grp == 0) {
-      f32x4 g = red[0][col];
-#pragma unroll
-      for (int q = 1; q < 16; ++q) g += red[q][col];
+      // the G group sums as a fixed pairwise tree: every LDS read issued at
+      // once, log2 G dependent adds (a chain over the groups waited on each read)
+      f32x4 g = red_tree<0, G>(red, col);
       MDP_STAMP(34);
       if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ctr_use(ep_raw) + 1u, &a.ctl->xw_ticks);
       double ss = 0.0;
@@ -476,18 +515,19 @@ extern "C" int mdp_debug_ra_wg(unsigned long long* t0, unsigned long long* t1, i
   } while (0)
 #endif
 
-__global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_reduce_apply(FusedApplyArgs f) {
   MDP_RA_WG(g_ra_t0);
   MDP_KARG_TOUCH("s"(f.pf_count), "s"(f.xstep), "s"(f.ap.blk[0]), "s"(f.ap.target), "s"(f.ap.clip), "s"(f.ap.stats_mode),
                  "s"(f.ap.ctl), "s"(gridDim.x), "s"(f.ap.net.t[0].off), "s"(f.ap.net.t[4].cols), "s"(f.ap.other.t[2].off),
                  "s"(f.ap.other.in));
   if (f.pf_count > 0 && blockIdx.x == gridDim.x - 1) {  // a piece of the next round's index draw
-    make_index_block<1024>(f.pf_ctl, f.pf_count, f.pf_out);
+    make_index_block<NT>(f.pf_ctl, f.pf_count, f.pf_out);
     __syncthreads();
     MDP_RA_WG(g_ra_t1);
     return;
   }
-  reduce_apply_body(f, blockIdx.x, gridDim.x - (f.pf_count > 0 ? 1 : 0));
+  reduce_apply_body<NT / 64>(f, blockIdx.x, gridDim.x - (f.pf_count > 0 ? 1 : 0));
 #ifdef MDP_STAMPS
   __syncthreads();
   MDP_RA_WG(g_ra_t1);
@@ -496,11 +536,12 @@ __global__ __launch_bounds__(1024) void k_reduce_apply(FusedApplyArgs f) {
 
 // throughput mode: the steps of several nets in one launch (each net's chunk
 // workgroups handshake only among themselves; the nets are independent)
-__global__ __launch_bounds__(1024) void k_reduce_apply_batch(RaBatch rb) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_reduce_apply_batch(RaBatch rb) {
   int q = 0;
   while (q + 1 < rb.count && (int)blockIdx.x >= rb.wg_start[q + 1]) ++q;
   const int b = blockIdx.x - rb.wg_start[q];
-  reduce_apply_body(rb.list[q], b, (uint32_t)(rb.wg_start[q + 1] - rb.wg_start[q]));
+  reduce_apply_body<NT / 64>(rb.list[q], b, (uint32_t)(rb.wg_start[q + 1] - rb.wg_start[q]));
 }
 
 int mdp_ra_grid(const FusedApplyArgs& f) {
@@ -508,23 +549,39 @@ int mdp_ra_grid(const FusedApplyArgs& f) {
   return f.rblk[6] + (a.polyak ? a.oblk[6] : 0) + (a.stats_mode ? 1 : 0);
 }
 
+// 256-thread workgroups (4 waves of up to 16 partials) when the fan-in is at
+// most 64 partials: S2 optimizer launch 3.88 -> 3.50 us event-timed (128
+// threads: 4.17, 512: 3.64).  MDP_RA_NARROW=0 builds the 1024-thread launch
+// for every fan-in (A/B only: its summation order differs)
+#ifndef MDP_RA_NARROW
+#define MDP_RA_NARROW 1
+#endif
+static bool mdp_ra_narrow(const FusedApplyArgs& f) { return MDP_RA_NARROW && f.ap.nwg <= 64; }
+
 hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_apply, dim3(mdp_ra_grid(f) + (f.pf_count > 0 ? 1 : 0)), dim3(1024), 0, s, f);
+  const dim3 grid(mdp_ra_grid(f) + (f.pf_count > 0 ? 1 : 0));
+  if (mdp_ra_narrow(f))
+    hipLaunchKernelGGL(k_reduce_apply<256>, grid, dim3(256), 0, s, f);
+  else
+    hipLaunchKernelGGL(k_reduce_apply<1024>, grid, dim3(1024), 0, s, f);
   return hipGetLastError();
 }
 
 // co-resident k_reduce_apply workgroups per CU
 hipError_t mdp_ra_occupancy(int* per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_reduce_apply, 1024, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_reduce_apply<1024>, 1024, 0);
 }
 
 // co-resident k_reduce_apply_batch workgroups per CU
 hipError_t mdp_ra_batch_occupancy(int* per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_reduce_apply_batch, 1024, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_reduce_apply_batch<1024>, 1024, 0);
 }
 
 hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_apply_batch, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
+  if (MDP_RA_NARROW && b.narrow)  // (no draw piece in a batch)
+    hipLaunchKernelGGL(k_reduce_apply_batch<256>, dim3(b.wg_start[b.count]), dim3(256), 0, s, b);
+  else
+    hipLaunchKernelGGL(k_reduce_apply_batch<1024>, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
   return hipGetLastError();
 }
 

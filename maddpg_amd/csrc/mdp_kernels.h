@@ -316,6 +316,7 @@ hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s);
 struct RaBatch {
   const FusedApplyArgs* list;
   int count;
+  int narrow;           // fan-in <= 64 partials: 256-thread workgroups (mdp_ra_narrow)
   int wg_start[MDP_RA_BATCH_MAX + 1];
 };
 int mdp_ra_grid(const FusedApplyArgs& f);

@@ -7,7 +7,7 @@ set -e
 NAME=$1; shift
 D=/tmp/mdp_variant_$NAME
 rm -rf $D; mkdir -p $D
-mkdir -p $D/maddpg_amd $D/include; cp -r maddpg_amd/csrc $D/maddpg_amd/csrc; cp include/*.h $D/include/
+mkdir -p $D/maddpg_amd $D/include $D/tools; cp -r maddpg_amd/csrc $D/maddpg_amd/csrc; cp include/*.h $D/include/; cp tools/check_scratch.py $D/tools/
 rm -rf $D/maddpg_amd/csrc/build
 make -s -C $D/maddpg_amd/csrc -j8 CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wall -Wno-unused-function $*" OUT=$D/lib.so HDR= > /dev/null
 cp $D/lib.so maddpg_amd/libmaddpg_hip_$NAME.so
