@@ -65,6 +65,9 @@ def parse_args(argv=None):
     parser.add_argument("--train-every", type=int, default=100, help="transitions per update round (maddpg.py:164)")
     parser.add_argument("--display-frames", type=int, default=100,
                         help="--display: steps rendered to PNG frames (no window on a GPU box)")
+    parser.add_argument("--save-format", choices=["npz", "tf1"], default="npz",
+                        help="checkpoint format: npz, or tf1 (a tf.train.Saver checkpoint with the reference's "
+                             "variable names; --load-dir reads either)")
     parser.add_argument("--update-mode", choices=["strict", "throughput"], default="strict",
                         help="strict: the reference's update order; throughput: every agent's gradients from "
                              "the round-start parameters, then every optimizer step (SURVEY 8e, single GPU)")
@@ -233,7 +236,7 @@ def train(arglist):
         steps = vec_steps * E
         points = curve.finish(E, runner.episode_rewards if rank == 0 else None)
         if points and rank == 0:
-            runner.eng.save_state(arglist.save_dir)
+            runner.eng.save_state(arglist.save_dir, arglist.save_format)
         for length, mean_ep, mean_ag in points:
             if rank != 0:
                 break

@@ -110,13 +110,15 @@ def initialize():
     return get_session().initialize()
 
 
-def save_state(fname, saver=None):
-    """U.save_state (tf_util.py:267-273): every variable of every agent."""
-    return get_session().engine().save_state(fname)
+def save_state(fname, saver=None, fmt="npz"):
+    """U.save_state (tf_util.py:267-273): every variable of every agent
+    (fmt="tf1": a TF1 checkpoint with the reference's variable names)."""
+    return get_session().engine().save_state(fname, fmt)
 
 
 def load_state(fname, saver=None):
-    """U.load_state (tf_util.py:259-264)."""
+    """U.load_state (tf_util.py:259-264): a TF1 checkpoint at prefix fname
+    (tf.train.Saver's files) or the .npz save_state writes."""
     return get_session().engine().load_state(fname)
 
 

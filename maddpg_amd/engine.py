@@ -225,7 +225,22 @@ class Engine:
             return os.path.join(fname, "maddpg_amd_state.npz")
         return fname + ".npz"
 
-    def save_state(self, fname):
+    def save_state(self, fname, fmt="npz"):
+        """fmt "npz": one .npz keyed like state_dict(); fmt "tf1": a TF1 tensor
+        bundle at prefix `fname` with the reference's variable names, as
+        tf.train.Saver().save(sess, fname) writes it (tf_util.py:267-273;
+        `fname`.index + `fname`.data-00000-of-00001 + the `checkpoint` state
+        file; no .meta -- the graph is built by code on both sides)."""
+        if fmt == "tf1":
+            from .common import tf_checkpoint as tfc
+            tfc.write_bundle(fname, tfc.tf1_from_state(self.state_dict()))
+            d = os.path.dirname(os.path.abspath(fname + "x"))
+            with open(os.path.join(d, "checkpoint"), "w") as fh:
+                p = os.path.abspath(fname) + ("/" if fname.endswith("/") else "")
+                fh.write(f'model_checkpoint_path: "{p}"\nall_model_checkpoint_paths: "{p}"\n')
+            return fname
+        if fmt != "npz":
+            raise ValueError(f"unknown checkpoint format {fmt!r} (npz, tf1)")
         path = self.checkpoint_path(fname)
         d = os.path.dirname(path)
         if d:
@@ -234,6 +249,13 @@ class Engine:
         return path
 
     def load_state(self, fname):
+        """Restore from a TF1 tensor bundle at prefix `fname` (the reference's
+        tf.train.Saver checkpoint, tf_util.py:259-264) when `fname`.index
+        exists, else from the .npz save_state writes."""
+        from .common import tf_checkpoint as tfc
+        if tfc.is_bundle(fname):
+            self.load_state_dict(tfc.state_from_tf1(tfc.read_bundle(fname), self.n, self.SETS))
+            return fname
         path = self.checkpoint_path(fname)
         with np.load(path, allow_pickle=False) as z:
             self.load_state_dict({k: z[k] for k in z.files})

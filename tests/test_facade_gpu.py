@@ -118,6 +118,19 @@ def test_trainer_facade_in_reference_loop(tmp_path):
         U.load_state(str(tmp_path) + "/")
         np.testing.assert_array_equal(eng.get_params(2, "tgt_critic")["W2"], before)
         assert os.path.exists(path)
+        # the same through a TF1 checkpoint (tf.train.Saver's files, the reference's names)
+        sd0 = eng.state_dict()
+        prefix = str(tmp_path) + "/tf1/"
+        U.save_state(prefix, fmt="tf1")
+        assert os.path.exists(prefix + ".index") and os.path.exists(prefix + ".data-00000-of-00001")
+        for w in eng.SETS:
+            eng.set_params(1, w, {k: v * 0 for k, v in eng.get_params(1, w).items()})
+        eng.set_beta_powers(1, 0, np.zeros(2, np.float32))
+        U.load_state(prefix)
+        sd1 = eng.state_dict()
+        assert sd0.keys() == sd1.keys()
+        for k in sd0:
+            np.testing.assert_array_equal(sd1[k], sd0[k], err_msg=k)
 
 
 @pytest.mark.parametrize("scenario,extra", [
@@ -125,6 +138,7 @@ def test_trainer_facade_in_reference_loop(tmp_path):
     ("simple_adversary", ["--num-adversaries", "1", "--adv-policy", "ddpg"]),
     ("simple_tag", ["--num-adversaries", "3"]),
     ("simple", []),
+    ("simple_spread", ["--save-format", "tf1"]),     # the reference's checkpoint files, restored below
 ])
 def test_train_cli_runs(tmp_path, capsys, scenario, extra):
     from experiments.train import parse_args, train
@@ -141,6 +155,9 @@ def test_train_cli_runs(tmp_path, capsys, scenario, extra):
     a2 = parse_args(["--scenario", scenario, "--num-envs", "64", "--num-episodes", "10", "--restore",
                      "--batch-size", "64", "--max-episode-len", "5", "--save-dir", str(tmp_path) + "/",
                      "--plots-dir", str(tmp_path) + "/", "--exp-name", "t2"] + extra)
+    if "tf1" in extra:
+        assert os.path.exists(str(tmp_path) + "/.index") and os.path.exists(str(tmp_path) + "/checkpoint")
+        assert not os.path.exists(str(tmp_path) + "/maddpg_amd_state.npz")
     train(a2)
     assert "Loading previous state..." in capsys.readouterr().out
 
