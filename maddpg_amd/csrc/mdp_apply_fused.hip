@@ -190,6 +190,8 @@ template <int G>
 __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const int b, const uint32_t nb) {
   const ApplyArgs& a = f.ap;
   __shared__ f32x4 red[G][64];
+  __shared__ f32x4 gl[64];         // the chunk's reduced gradient (wave 0 -> the Adam waves)
+  __shared__ float step_l[4];      // beta1^t, beta2^t, the tensor norm, fault
   const int tid = threadIdx.x, lane = tid & 63;
   MDP_STAMP(30);
   if (f.phase == 1 && b >= f.rblk[6]) return;  // reduce-only pass: chunk workgroups only
@@ -204,9 +206,15 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     const int p0 = c * MDP_RA_CHUNK + 4 * col;  // this thread's 4 parameters (tensor-relative)
     const bool act = p0 < n;
     const int64_t i0 = td.off + p0;             // absolute parameter index
-    // Adam state of the chunk, requested with the partial-gradient loads
-    f32x4 m4 = {0.f, 0.f, 0.f, 0.f}, v4 = m4, th4 = m4, tg4 = m4;
-    const float b1p = a.beta[0], b2p = a.beta[1];  // this step's powers (advanced at the end)
+    // The Adam step runs on waves 0..3, wave q on parameters 64 q .. 64 q + 63
+    // of the chunk (one per lane, contiguous): on wave 0 alone, four parameters
+    // per lane of divides and square roots took 0.7 us of VALU issue (stamped).
+    // Its state is requested with the partial-gradient loads.
+    const int pq = c * MDP_RA_CHUNK + 64 * grp + lane;
+    const bool aact = grp < 4 && pq < n;
+    const int64_t iq = td.off + pq;
+    float m1 = 0.f, v1 = 0.f, th1 = 0.f, tg1 = 0.f;
+    const float b1p = a.beta[0], b2p = a.beta[1];  // this step's powers (wave 0; advanced at the end)
     // exchange epoch (advanced at the end); kept opaque until the exchange --
     // the +1 here made the compiler wait for the load in front of the partials
     const uint32_t ep_raw = f.phase == 3 ? f.xstep[0] : 0u;
@@ -218,11 +226,11 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     uint32_t fault0 = 0u;
     if (grp == 0) fault0 = __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool faulted = false;
-    if (grp == 0 && act) {
-      m4 = ld4(a.m + i0);
-      v4 = ld4(a.v + i0);
-      th4 = ld4(a.theta + i0);
-      if (a.polyak) tg4 = ld4(a.target + i0);
+    if (aact && f.phase != 1) {
+      m1 = a.m[iq];
+      v1 = a.v[iq];
+      th1 = a.theta[iq];
+      if (a.polyak) tg1 = a.target[iq];
     }
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     if constexpr (G == 16) {
@@ -342,40 +350,39 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       if (f.phase == 3)
         faulted = faulted || __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
       MDP_STAMP(37);
-      if (act && !faulted) {
-        const float norm = (float)sqrt(tot);
+      // the chunk's gradient, this step's powers, the norm and the fault state
+      // to the Adam waves
+      gl[col] = g;
+      if (lane == 0) {
+        step_l[0] = b1p;
+        step_l[1] = b2p;
+        step_l[2] = (float)sqrt(tot);
+        step_l[3] = faulted ? 1.f : 0.f;
+      }
+      }  // phase != 1
+    }
+    if (f.phase != 1) {
+      __syncthreads();
+      // TF1 ApplyAdam (+ Polyak for the actor step) of this lane's parameter
+      // (a timed-out handshake of this chunk, exchange of this launch or an
+      // earlier launch's fault leaves the optimizer state as it was)
+      if (aact && step_l[3] == 0.f) {
+        const float gq = reinterpret_cast<const float*>(gl)[64 * grp + lane];
+        const float norm = step_l[2];
         const float clip = a.clip;
         const float denom = fmaxf(norm, clip);
         const float one = 1.0f;
-        const float alpha = a.lr * sqrtf(one - b2p) / (one - b1p);
+        const float alpha = a.lr * sqrtf(one - step_l[1]) / (one - step_l[0]);
         const float c1 = one - a.b1, c2 = one - a.b2;
-        f32x4 mo, vo, tho, tgo;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float gc = ((g[j] * a.scale) * clip) / denom;
-          mo[j] = m4[j] + (gc - m4[j]) * c1;
-          vo[j] = v4[j] + (gc * gc - v4[j]) * c2;
-          tho[j] = th4[j] - (mo[j] * alpha) / (sqrtf(vo[j]) + a.eps);
-          tgo[j] = a.pa * tg4[j] + a.pb * tho[j];
-        }
-        if (p0 + 3 < n) {  // the whole float4 in the tensor: one 16-B store per array
-          *reinterpret_cast<f32x4*>(a.m + i0) = mo;
-          *reinterpret_cast<f32x4*>(a.v + i0) = vo;
-          *reinterpret_cast<f32x4*>(a.theta + i0) = tho;
-          if (a.polyak) *reinterpret_cast<f32x4*>(a.target + i0) = tgo;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (p0 + j < n) {
-              a.m[i0 + j] = mo[j];
-              a.v[i0 + j] = vo[j];
-              a.theta[i0 + j] = tho[j];
-              if (a.polyak) a.target[i0 + j] = tgo[j];
-            }
-          }
-        }
+        const float gc = ((gq * a.scale) * clip) / denom;
+        const float mo = m1 + (gc - m1) * c1;
+        const float vo = v1 + (gc * gc - v1) * c2;
+        const float tho = th1 - (mo * alpha) / (sqrtf(vo) + a.eps);
+        a.m[iq] = mo;
+        a.v[iq] = vo;
+        a.theta[iq] = tho;
+        if (a.polyak) a.target[iq] = a.pa * tg1 + a.pb * tho;
       }
-      }  // phase != 1
     }
   } else if (a.polyak && b < f.rblk[6] + a.oblk[6]) {
     if (__hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
@@ -518,6 +525,7 @@ extern "C" int mdp_debug_ra_wg(unsigned long long* t0, unsigned long long* t1, i
 template <int NT>
 __global__ __launch_bounds__(NT) void k_reduce_apply(FusedApplyArgs f) {
   MDP_RA_WG(g_ra_t0);
+  MDP_TL(f.ap.ctl, f.ap.polyak ? 3 : 1, blockIdx.x == gridDim.x - 1 && f.pf_count > 0 ? 3 : 0);
   MDP_KARG_TOUCH("s"(f.pf_count), "s"(f.xstep), "s"(f.ap.blk[0]), "s"(f.ap.target), "s"(f.ap.clip), "s"(f.ap.stats_mode),
                  "s"(f.ap.ctl), "s"(gridDim.x), "s"(f.ap.net.t[0].off), "s"(f.ap.net.t[4].cols), "s"(f.ap.other.t[2].off),
                  "s"(f.ap.other.in));
@@ -584,6 +592,18 @@ hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s) {
     hipLaunchKernelGGL(k_reduce_apply_batch<1024>, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
   return hipGetLastError();
 }
+
+#ifdef MDP_TIMELINE
+extern "C" int mdp_debug_tl_ra(unsigned long long* out, int reset) {
+  const size_t n = sizeof(unsigned long long) * MDP_TL_SLOTS * MDP_TL_WG * 2;
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_mdp_tl)) != hipSuccess) return -1;
+    return hipMemset(p, 0, n) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_tl), n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef MDP_STAMPS
 // diagnostic build: stamps of this translation unit's kernels (own code object)

@@ -49,6 +49,48 @@ __device__ unsigned long long g_mdp_stamps[64];
   } while (0)
 #endif
 
+// diagnostic build only (-DMDP_TIMELINE, `make timeline`): per launch of a
+// round, the first workgroup start and the last wave end (s_memrealtime, 100
+// MHz), keyed by the update counter at entry (one agent update: critic launch,
+// its optimizer, actor launch, its optimizer) and the workgroup's role -- the
+// graph-replayed round's launch bodies and the gaps between them
+// (tools/timeline.py).  Slot = (upd_ctr & 255) * 16 + 4 * kind + role.
+#ifdef MDP_TIMELINE
+// per (slot, workgroup): start (thread 0, plain store) and end (max over the
+// workgroup's waves: an atomic on a per-workgroup word, so at most 16 waves
+// contend -- one word per slot made ~1000 waves queue on one address)
+#define MDP_TL_SLOTS 1024
+#define MDP_TL_WG 512
+__device__ unsigned long long g_mdp_tl[MDP_TL_SLOTS][MDP_TL_WG][2];
+struct MdpTl {
+  unsigned long long t0;
+  uint32_t ctr;
+  int kr;
+  __device__ MdpTl(const uint32_t* upd_ctr, int kind, int role)
+      : t0(__builtin_amdgcn_s_memrealtime()),
+        ctr(__hip_atomic_load(const_cast<uint32_t*>(upd_ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+        kr(4 * kind + role) {}
+  __device__ void set_role(int kind, int role) { kr = 4 * kind + role; }
+  __device__ ~MdpTl() {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t slot = (ctr & 63u) * 16u + (uint32_t)kr;
+    if (blockIdx.x < MDP_TL_WG) {
+      if (threadIdx.x == 0) g_mdp_tl[slot][blockIdx.x][0] = t0;
+      if ((threadIdx.x & 63) == 0) atomicMax(&g_mdp_tl[slot][blockIdx.x][1], t1);
+    }
+  }
+};
+#define MDP_TL(ctl, kind, role) MdpTl mdp_tl_(&(ctl)->upd_ctr, kind, role)
+#define MDP_TL_ROLE(kind, role) mdp_tl_.set_role(kind, role)
+#else
+#define MDP_TL(ctl, kind, role) \
+  do {                          \
+  } while (0)
+#define MDP_TL_ROLE(kind, role) \
+  do {                          \
+  } while (0)
+#endif
+
 // A kernel's first branches each read a kernarg field, and the compiler issues
 // each read behind the previous branch: a chain of scalar-cache misses (ISA:
 // five s_load / s_waitcnt pairs before the first global load).  Naming one

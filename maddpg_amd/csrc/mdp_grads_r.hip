@@ -387,7 +387,9 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   MDP_KARG_TOUCH("s"(a.agent), "s"(a.inv_b), "s"(a.pf_count), "s"(a.cpre_prev), "s"(a.topo.n), "s"(gridDim.x));
   MDP_WG_START(0);
+  MDP_TL(a.ctl, 0, 0);
   if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
+    MDP_TL_ROLE(0, 2);
     // the next round's index draw (same ring length, the MT stream continues):
     // one workgroup beside the B/16 of this kernel, so it costs no time of its own
     make_index_block<512>(a.pf_ctl, a.pf_count, a.pf_out);
@@ -397,10 +399,12 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;  // gather waves done (LDS hand-off, replaces a barrier)
   __shared__ int post_sync[2];  // critic_post: target-actor L1, L2 tiles of waves 0..3 done
+  __shared__ int dq_ready;      // wave 4 wrote dL/dq (the dh1 tiles of waves 0..3 wait for it)
   int agent = a.agent, bx = blockIdx.x;
   if (a.apre) {  // workgroups [B/16, 2 B/16): the actor step's forward (strict mode only)
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
     if (bx >= nwg) {
+      MDP_TL_ROLE(0, 1);
       actor_pre_tile(a, lds, &rows_ready, bx - nwg);
       MDP_WG_END(0);
       return;
@@ -459,10 +463,12 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   MDP_STAMP(0);
   if (threadIdx.x == 0) rows_ready = 0;
   if (threadIdx.x < 2) post_sync[threadIdx.x] = 0;
+  if (threadIdx.x == 2) dq_ready = 0;
   __syncthreads();  // B0 (nothing in flight yet)
 
   if (wave < 4) {
     f32x4 wt[4];  // W2^T tile of the critic for dh1 (loaded once this wave's forward weights are dead)
+    float w3v;    // W3 of the critic at column `lane` (v = W3 o [h2c > 0], below)
     if (post) {
       // ---------------- critic_post: target actor pprev (Polyak-updated since the
       // critic_pre) over waves 0..3, one 16-column tile of L1 and L2 each, the
@@ -511,6 +517,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         gumbel_noise5(u, gn);
       }
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      w3v = Pc[nd.t[4].off + lane];
       float* h1 = h1a;
       float* h2 = h2a;
       if (wave == 0) MDP_STAMPW(48);
@@ -635,6 +642,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       MDP_STAMP(2);
       MDP_CLK(44);
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      w3v = Pc[nd.t[4].off + lane];
       __syncthreads();  // B2
     } else if (wave == 3) {
       // ---------------- online critic forward q(o, a) (maddpg.py:85-88, 104)
@@ -664,19 +672,40 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       wave_sync();
       MDP_STAMPW(3);
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      w3v = Pc[nd.t[4].off + lane];
       __syncthreads();  // B2
       const float q = rq_head(h2c, LH, w3) + b3;
       if ((lane & 3) == 0) qv[lane >> 2] = q;
     } else {
       rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
+      w3v = Pc[nd.t[4].off + lane];
       __syncthreads();  // B2
     }
+    // The critic backward is linear in the per-row dL/dq (maddpg.py:91):
+    // d2 = dq o v with v = W3 o [h2c > 0], dh1 = dq o u with u = (v W2^T) o
+    // [h1c > 0].  u needs no TD target, so waves 0..3 compute it while waves
+    // 4..7 run the target critic and the TD error, and scale it by dq once wave
+    // 4 has it: the dh1 tiles leave the critical path and dW2, dW1 run as one
+    // phase after B5.  v (rows 4 wave .. 4 wave + 3) in the d2 buffer until
+    // wave 4 overwrites it with dq o v after B4.
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = 4 * wave + i;
+      d2[rr * LD + lane] = h2c[rr * LH + lane] > 0.f ? w3v : 0.f;
+    }
     __syncthreads();  // B3
+    const f32x4 u = rdg_acc(d2, LD, wt);  // u tile `wave` (columns 16 wave .. 16 wave + 15)
     __syncthreads();  // B4
-    __syncthreads();  // B5: d2 ready
-    dgrad_tile(d2, wt, h1c, d1, wave);
-    wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 0, 8);
-    __syncthreads();  // B6
+    lds_wait(&dq_ready, 1);
+    {
+      const int col = 16 * wave + r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = kq * 4 + i;
+        d1[row * LD + col] = h1c[row * LH + col] > 0.f ? dq[row] * u[i] : 0.f;
+      }
+    }
+    __syncthreads();  // B5: d2, d1 ready
   } else {
     // ---------------- target critic Q'(o', a~), one 16-column tile per wave
     const int tt = wave - 4, col = 16 * tt + r;
@@ -746,6 +775,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         y_out[r0 + lane] = y64;
       }
       if (lane < MDP_R) dq[lane] = g;
+      lds_signal(&dq_ready);
       MDP_STAMPW(60);
       wave_sync();
       // dW3 = h2^T dq, db3 = sum dq, d2 = (dq W3^T) o [h2 > 0]   (lane = hidden unit)
@@ -778,13 +808,11 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         st[3] = s_q;
       }
     }
-    // dW2 = h1^T d2 over all waves (tiles w, w + 8; waves 0..3 after their dh1 tile), db2
-    wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 0, 8);
-    if (tt == 1) colsum64(d2, LD, slab + nd.t[3].off);
-    __syncthreads();  // B6
-    if (tt == 0) MDP_STAMPW(9);
   }
-  // dW1 = x^T dh1 over all waves, db1 = column sums of dh1
+  // one phase: dW2 = h1^T d2 (tiles w, w + 8), db2, dW1 = x^T dh1, db1 = column sums of dh1
+  wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 0, 8);
+  if (wave == 5) colsum64(d2, LD, slab + nd.t[3].off);
+  if (wave == 4) MDP_STAMPW(9);
   wgrad_waves(rowbuf + xo_c, ldr, ka_c, d1, LD, RH, slab + nd.t[0].off, 0, 8);
   if (kb_c) wgrad_waves(rowbuf + ag.act_off, ldr, kb_c, d1, LD, RH, slab + nd.t[0].off + ka_c * RH, 0, 8);
   if (wave == 7) colsum64(d1, LD, slab + nd.t[1].off);
@@ -798,10 +826,12 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   __shared__ int rows_ready;
   __shared__ int fwd_issued;  // waves 0..3 issued the loads the critic forward needs first
   MDP_WG_START(1);
+  MDP_TL(a.ctl, 2, 0);
   int agent = a.agent, bx = blockIdx.x;
   if (a.cpre) {  // workgroups [B/16, 2 B/16): the next critic step's independent work (strict mode)
     const int nwg = (a.B + MDP_R - 1) / MDP_R;
     if (bx >= nwg) {
+      MDP_TL_ROLE(2, 1);
       critic_pre_tile(a, lds, &rows_ready, bx - nwg);
       MDP_WG_END(1);
       return;
@@ -1059,6 +1089,18 @@ hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_
   // grid: actor row tiles | the next critic step's row tiles (a.cpre)
   return launch_r(k_actor_grad_r, a, lds_bytes, s, attr, a.cpre ? (a.B + MDP_R - 1) / MDP_R : 0);
 }
+
+#ifdef MDP_TIMELINE
+extern "C" int mdp_debug_tl_r(unsigned long long* out, int reset) {
+  const size_t n = sizeof(unsigned long long) * MDP_TL_SLOTS * MDP_TL_WG * 2;
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_mdp_tl)) != hipSuccess) return -1;
+    return hipMemset(p, 0, n) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_tl), n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef MDP_STAMPS
 // diagnostic build: stamps of this translation unit's kernels (own code object)
