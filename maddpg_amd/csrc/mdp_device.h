@@ -1079,6 +1079,75 @@ __device__ __forceinline__ void slab_st(float* p, float v) {
   *p = v;
 #endif
 }
+// One weight-gradient job of wgrad_multi: dW[K][N] (global, stride N) of
+// X^T[K][16] dY[16][N] (LDS operands); K = 0: no job
+struct WgJob {
+  const float* X;
+  const float* dY;
+  float* dW;
+  int ldx, K, ldy, N;
+};
+// The tiles of up to three jobs, concatenated and dealt round-robin over waves
+// [w0, w0 + wn).  A wave reads the LDS operands of T tiles at once and runs
+// their MFMA chains interleaved before storing: one tile at a time, each
+// 4-step chain waited on its LDS reads and on itself (40-cycle dependent MFMA
+// latency), ~0.3 us per tile.  Each tile's chain is wgrad_waves' (same k
+// order), so the result is bit-identical.  Tiles past the end re-read a valid
+// tile (clamped) and store nothing.
+template <int T>
+__device__ __forceinline__ void wgrad_multi(const WgJob& j0, const WgJob& j1, const WgJob& j2, int w0, int wn) {
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave < w0 || wave >= w0 + wn) return;
+  const int r = lane & 15, kq = lane >> 4;
+  const int n0 = ((j0.K + 15) >> 4) * (j0.N >> 4);
+  const int n1 = j1.K > 0 ? ((j1.K + 15) >> 4) * (j1.N >> 4) : 0;
+  const int n2 = j2.K > 0 ? ((j2.K + 15) >> 4) * (j2.N >> 4) : 0;
+  const int total = n0 + n1 + n2;
+  for (int base = wave - w0; base < total; base += T * wn) {
+    float a[T][4], g[T][4];
+    float* dst[T];
+    int krem[T], nstr[T];
+#pragma unroll
+    for (int s = 0; s < T; ++s) {
+      const int tv = base + s * wn;
+      const int t = min(tv, total - 1);
+      const bool in0 = t < n0, in1 = !in0 && t < n0 + n1;
+      const float* X = in0 ? j0.X : (in1 ? j1.X : j2.X);
+      const float* dY = in0 ? j0.dY : (in1 ? j1.dY : j2.dY);
+      float* dW = in0 ? j0.dW : (in1 ? j1.dW : j2.dW);
+      const int ldx = in0 ? j0.ldx : (in1 ? j1.ldx : j2.ldx);
+      const int K = in0 ? j0.K : (in1 ? j1.K : j2.K);
+      const int ldy = in0 ? j0.ldy : (in1 ? j1.ldy : j2.ldy);
+      const int N = in0 ? j0.N : (in1 ? j1.N : j2.N);
+      const int tl = in0 ? t : (in1 ? t - n0 : t - n0 - n1);
+      const int nnt = N >> 4, mt = tl / nnt, nt = tl - mt * nnt;
+      const int feat = mt * 16 + r, fc = min(feat, K - 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 4 * i + kq;
+        const float xv = X[row * ldx + fc];
+        a[s][i] = feat < K ? xv : 0.f;
+        g[s][i] = dY[row * ldy + nt * 16 + r];
+      }
+      dst[s] = dW + (mt * 16 + kq * 4) * N + nt * 16 + r;
+      krem[s] = tv < total ? K - (mt * 16 + kq * 4) : 0;
+      nstr[s] = N;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every LDS read ahead of the MFMA chains
+    f32x4 acc[T];
+#pragma unroll
+    for (int s = 0; s < T; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < T; ++s) acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][i], g[s][i], acc[s], 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < T; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < krem[s]) slab_st(dst[s] + i * nstr[s], acc[s][i]);
+  }
+}
 __device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, const float* dY, int ldy, int N,
                                             float* __restrict__ dW, int w0, int wn) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

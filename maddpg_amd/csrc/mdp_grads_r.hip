@@ -809,12 +809,16 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       }
     }
   }
-  // one phase: dW2 = h1^T d2 (tiles w, w + 8), db2, dW1 = x^T dh1, db1 = column sums of dh1
+  // one phase: dW2 = h1^T d2, dW1 = x^T dh1, db2 and db1 = column sums of d2, dh1
+  // (wgrad_multi here -- every tile's operands read first, the chains
+  // interleaved, stores last -- measured slower: S2 1.074M -> 1.048M with all
+  // five tiles of a wave at once, 1.064M as 2 + 3: the stores of the first
+  // tiles no longer drain behind the later tiles' work)
   wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 0, 8);
-  if (wave == 5) colsum64(d2, LD, slab + nd.t[3].off);
-  if (wave == 4) MDP_STAMPW(9);
   wgrad_waves(rowbuf + xo_c, ldr, ka_c, d1, LD, RH, slab + nd.t[0].off, 0, 8);
   if (kb_c) wgrad_waves(rowbuf + ag.act_off, ldr, kb_c, d1, LD, RH, slab + nd.t[0].off + ka_c * RH, 0, 8);
+  if (wave == 4) MDP_STAMPW(9);
+  if (wave == 5) colsum64(d2, LD, slab + nd.t[3].off);
   if (wave == 7) colsum64(d1, LD, slab + nd.t[1].off);
   MDP_STAMP(10);
   MDP_WG_END(0);
@@ -1028,8 +1032,9 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       d2a_rows(h2a, dl, w3a, d2a, gwpart, wave);
       __syncthreads();  // B5
     }
-    // dW2a = h1a^T d2a (waves 0..3), db2a
-    wgrad_waves(h1a, LH, RH, d2a, LD, RH, slab + na.t[2].off, 0, 4);
+    // dW2a = h1a^T d2a (waves 0..3, four tiles each, interleaved), db2a
+    wgrad_multi<4>(WgJob{h1a, d2a, slab + na.t[2].off, LH, RH, LD, RH}, WgJob{nullptr, nullptr, nullptr, 0, 0, 0, 64},
+                   WgJob{nullptr, nullptr, nullptr, 0, 0, 0, 64}, 0, 4);
     if (wave == 3) colsum64(d2a, LD, slab + na.t[3].off);
     __syncthreads();  // B6
   } else {
