@@ -467,7 +467,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   __syncthreads();  // B0 (nothing in flight yet)
 
   if (wave < 4) {
-    f32x4 wt[4];  // W2^T tile of the critic for dh1 (loaded once this wave's forward weights are dead)
+    f32x4 wt[4];  // W2^T tile of the critic for u (requested after B2, off the prologue's load burst)
     float w3v;    // W3 of the critic at column `lane` (v = W3 o [h2c > 0], below)
     if (post) {
       // ---------------- critic_post: target actor pprev (Polyak-updated since the
@@ -476,32 +476,18 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       const ADesc& aj = T.ag[pprev];
       const NDesc& an = aj.actor;
       const int col = 16 * wave + r;
+      // the cpre block, issued first (wave 1 h1c, wave 2 h2c, wave 3 q and the
+      // a~ except pprev's) but written to LDS only after this wave's L2 tile:
+      // written here, each wave waited for its block before issuing its
+      // target-actor weights, which then landed ~1 us after wave 0's
+      const int c0 = wave == 1 ? 0 : (wave == 2 ? 64 : 192), nc4 = wave == 3 ? 5 : 16;
+      f32x4 cv4[4];
       if (wave > 0) {
-        // the cpre block, issued first: wave 1 h1c, wave 2 h2c, wave 3 q and the a~ (not pprev's)
         const float* src = a.cpre + (int64_t)r0 * MDP_CPRE_W;
-        const int c0 = wave == 1 ? 0 : (wave == 2 ? 64 : 192), nc4 = wave == 3 ? 5 : 16;
-        f32x4 v[4];
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
           const int q = min(lane + 64 * it, MDP_R * nc4 - 1), row = q / nc4;
-          v[it] = ld4(src + (int64_t)row * MDP_CPRE_W + c0 + 4 * (q - row * nc4));
-        }
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          const int q = lane + 64 * it, row = q / nc4, c = c0 + 4 * (q - row * nc4);
-          if (q < MDP_R * nc4) {
-            if (c < 64) *reinterpret_cast<f32x4*>(h1c + row * LH + c) = v[it];
-            else if (c < 128) *reinterpret_cast<f32x4*>(h2c + row * LH + c - 64) = v[it];
-            else if (c == 192) qv[row] = v[it][0];
-            else {  // the stored target actions (not pprev's slot: wave 0 writes it)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int cc = c - 196 + e;
-                if (cc < kb && (cc < MDP_ACT_DIM * pprev || cc >= MDP_ACT_DIM * (pprev + 1)))
-                  xa[row * ldA + cc] = v[it][e];
-              }
-            }
-          }
+          cv4[it] = ld4(src + (int64_t)row * MDP_CPRE_W + c0 + 4 * (q - row * nc4));
         }
       }
       float w1t[16], w2t[16], w3[16];
@@ -516,7 +502,6 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
         uniforms5(a.seed, (uint32_t)((agent << 8) | (pprev + 1)), ctr_use(ctr), (uint32_t)(r0 + (lane & 15)), u);
         gumbel_noise5(u, gn);
       }
-      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       w3v = Pc[nd.t[4].off + lane];
       float* h1 = h1a;
       float* h2 = h2a;
@@ -537,6 +522,25 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       lds_signal(&post_sync[1]);
       if (wave == 0) MDP_STAMPW(50);
       if (wave == 3) MDP_STAMPW(55);
+      if (wave > 0) {  // the cpre block into LDS (landed with the weights: loads complete in order)
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int q = lane + 64 * it, row = q / nc4, c = c0 + 4 * (q - row * nc4);
+          if (q < MDP_R * nc4) {
+            if (c < 64) *reinterpret_cast<f32x4*>(h1c + row * LH + c) = cv4[it];
+            else if (c < 128) *reinterpret_cast<f32x4*>(h2c + row * LH + c - 64) = cv4[it];
+            else if (c == 192) qv[row] = cv4[it][0];
+            else {  // the stored target actions (not pprev's slot: wave 0 writes it)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int cc = c - 196 + e;
+                if (cc < kb && (cc < MDP_ACT_DIM * pprev || cc >= MDP_ACT_DIM * (pprev + 1)))
+                  xa[row * ldA + cc] = cv4[it][e];
+              }
+            }
+          }
+        }
+      }
       if (wave == 0) {
         lds_wait(&post_sync[1], 4);
         MDP_STAMPW(51);
@@ -641,7 +645,6 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       }
       MDP_STAMP(2);
       MDP_CLK(44);
-      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       w3v = Pc[nd.t[4].off + lane];
       __syncthreads();  // B2
     } else if (wave == 3) {
@@ -671,13 +674,11 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
       }
       wave_sync();
       MDP_STAMPW(3);
-      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       w3v = Pc[nd.t[4].off + lane];
       __syncthreads();  // B2
       const float q = rq_head(h2c, LH, w3) + b3;
       if ((lane & 3) == 0) qv[lane >> 2] = q;
     } else {
-      rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
       w3v = Pc[nd.t[4].off + lane];
       __syncthreads();  // B2
     }
@@ -688,14 +689,27 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     // 4 has it: the dh1 tiles leave the critical path and dW2, dW1 run as one
     // phase after B5.  v (rows 4 wave .. 4 wave + 3) in the d2 buffer until
     // wave 4 overwrites it with dq o v after B4.
+    // The W2^T tile is requested only here: issued with the prologue's loads it
+    // competed with the target actor's weights on the critical path, and u is
+    // needed only once wave 4 has dq (after B4).
+    rdg_load(wt, Pc + nd.t[2].off, 16 * wave + r, true);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rr = 4 * wave + i;
       d2[rr * LD + lane] = h2c[rr * LH + lane] > 0.f ? w3v : 0.f;
     }
     __syncthreads();  // B3
-    const f32x4 u = rdg_acc(d2, LD, wt);  // u tile `wave` (columns 16 wave .. 16 wave + 15)
+    float vx[16];  // this lane's v fragments (row lane & 15), read before wave 4 overwrites d2
+    {
+      const float* yr = d2 + r * LD + 16 * kq;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) vx[q] = yr[q];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();  // B4
+    f32x4 u = {0.f, 0.f, 0.f, 0.f};  // u tile `wave` (columns 16 wave .. 16 wave + 15), rdg_acc's chain
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u = __builtin_amdgcn_mfma_f32_16x16x4f32(vx[q], wt[q >> 2][q & 3], u, 0, 0, 0);
     lds_wait(&dq_ready, 1);
     {
       const int col = 16 * wave + r;
