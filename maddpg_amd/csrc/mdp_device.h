@@ -299,32 +299,6 @@ __device__ __forceinline__ void tile_fwd(const float* X, int ldx, int K, const f
   }
 }
 
-// dW[K][N] = X^T[K][16] @ dY[16][N], written to global (row-major, stride N).
-// Rows >= K are not written.
-__device__ __forceinline__ void tile_wgrad(const float* X, int ldx, int K, const float* dY, int ldy, int N,
-                                  float* __restrict__ dW) {
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 15, kq = lane >> 4;
-  const int nmt = (K + 15) >> 4, nnt = N >> 4;
-  for (int t = wave; t < nmt * nnt; t += MDP_NW) {
-    const int mt = t / nnt, nt = t - mt * nnt;
-    const int feat = mt * 16 + r;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r0 = 0; r0 < MDP_R; r0 += 4) {
-      const int row = r0 + kq;
-      const float a = feat < K ? X[row * ldx + feat] : 0.f;
-      const float g = dY[row * ldy + nt * 16 + r];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = mt * 16 + kq * 4 + i;
-      if (k < K) dW[k * N + nt * 16 + r] = acc[i];
-    }
-  }
-}
-
 // dX[16][K] = (dY[16][N] @ W^T) masked by (H > 0) where H is the layer input
 // (post-ReLU activations of the previous layer); K multiple of 16.
 __device__ __forceinline__ void tile_dgrad_relu(const float* dY, int ldy, int N, const float* __restrict__ W, int K,
@@ -727,33 +701,6 @@ __device__ __forceinline__ void wave_dgrad(const float* dY, int ldy, int N, cons
   wave_sync();
 }
 
-// dW tiles (M = K_feat rows of X^T, N = H) written to global, over the waves
-// starting at wave offset w0 (so the long dgrad chains can take other waves).
-__device__ __forceinline__ void wgrad_tiles(const float* X, int ldx, int K, const float* dY, int ldy, int N,
-                                   float* __restrict__ dW, int w0) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int r = lane & 15, kq = lane >> 4;
-  const int nmt = (K + 15) >> 4, nnt = N >> 4;
-  const int wv = (wave - w0 + nw) % nw;
-  for (int t = wv; t < nmt * nnt; t += nw) {
-    const int mt = t / nnt, nt = t - mt * nnt;
-    const int feat = mt * 16 + r;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r0 = 0; r0 < MDP_R; r0 += 4) {
-      const int row = r0 + kq;
-      const float a = feat < K ? X[row * ldx + feat] : 0.f;
-      const float g = dY[row * ldy + nt * 16 + r];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = mt * 16 + kq * 4 + i;
-      if (k < K) dW[k * N + nt * 16 + r] = acc[i];
-    }
-  }
-}
-
 // dX[16][K] = (dY[16][N] @ W^T) masked by Hin > 0, tiles over waves 0..K/16-1
 // (the caller keeps those waves free of other work); W global [K][N].
 __device__ __forceinline__ void dgrad_tiles(const float* dY, int ldy, int N, const float* __restrict__ W, int K,
@@ -1079,6 +1026,21 @@ __device__ __forceinline__ void slab_st(float* p, float v) {
   *p = v;
 #endif
 }
+__device__ __forceinline__ void slab_st4(float* p, f32x4 v) {
+#if MDP_NT_SLAB == 2
+#pragma unroll
+  for (int j = 0; j < 4; ++j) __hip_atomic_store(p + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif MDP_NT_SLAB
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+#else
+  *reinterpret_cast<f32x4*>(p) = v;
+#endif
+}
+// Weight-gradient tiles are computed TRANSPOSED, dW^T tile = dY^T X (the
+// MFMA's A operand from dY, B from X -- the same products in the same k
+// order, so every element is bit-identical to the X^T dY form): a lane then
+// holds dW[k][n .. n + 3] for one k, written as ONE 16-byte store instead of
+// four 4-byte stores to four rows (N and the tensor offsets are multiples of 4).
 // One weight-gradient job of wgrad_multi: dW[K][N] (global, stride N) of
 // X^T[K][16] dY[16][N] (LDS operands); K = 0: no job
 struct WgJob {
@@ -1106,7 +1068,7 @@ __device__ __forceinline__ void wgrad_multi(const WgJob& j0, const WgJob& j1, co
   for (int base = wave - w0; base < total; base += T * wn) {
     float a[T][4], g[T][4];
     float* dst[T];
-    int krem[T], nstr[T];
+    bool krem[T];
 #pragma unroll
     for (int s = 0; s < T; ++s) {
       const int tv = base + s * wn;
@@ -1129,9 +1091,8 @@ __device__ __forceinline__ void wgrad_multi(const WgJob& j0, const WgJob& j1, co
         a[s][i] = feat < K ? xv : 0.f;
         g[s][i] = dY[row * ldy + nt * 16 + r];
       }
-      dst[s] = dW + (mt * 16 + kq * 4) * N + nt * 16 + r;
-      krem[s] = tv < total ? K - (mt * 16 + kq * 4) : 0;
-      nstr[s] = N;
+      dst[s] = dW + feat * N + nt * 16 + kq * 4;
+      krem[s] = tv < total && feat < K;
     }
     __builtin_amdgcn_sched_barrier(0);  // every LDS read ahead of the MFMA chains
     f32x4 acc[T];
@@ -1140,12 +1101,10 @@ __device__ __forceinline__ void wgrad_multi(const WgJob& j0, const WgJob& j1, co
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < T; ++s) acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][i], g[s][i], acc[s], 0, 0, 0);
+      for (int s = 0; s < T; ++s) acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(g[s][i], a[s][i], acc[s], 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < T; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (i < krem[s]) slab_st(dst[s] + i * nstr[s], acc[s][i]);
+      if (krem[s]) slab_st4(dst[s], acc[s]);
   }
 }
 __device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, const float* dY, int ldy, int N,
@@ -1165,13 +1124,9 @@ __device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, cons
       const float xv = X[row * ldx + fc];
       const float a = feat < K ? xv : 0.f;
       const float g = dY[row * ldy + nt * 16 + r];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(g, a, acc, 0, 0, 0);  // transposed tile
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = mt * 16 + kq * 4 + i;
-      if (k < K) slab_st(dW + k * N + nt * 16 + r, acc[i]);
-    }
+    if (feat < K) slab_st4(dW + feat * N + nt * 16 + kq * 4, acc);
   }
 }
 

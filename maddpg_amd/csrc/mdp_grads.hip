@@ -460,13 +460,9 @@ __device__ __forceinline__ void wgrad_tile(const float* X, int ldx, int K, const
     const float xv = X[row * ldx + fc];
     const float a = feat < K ? xv : 0.f;
     const float g = dY[row * ldy + nt * 16 + r];
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(g, a, acc, 0, 0, 0);  // transposed tile (slab_st4)
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int k = mt * 16 + kq * 4 + i;
-    if (k < K) slab_st(dW + k * N + nt * 16 + r, acc[i]);
-  }
+  if (feat < K) slab_st4(dW + feat * N + nt * 16 + kq * 4, acc);
 }
 }  // namespace
 
