@@ -20,9 +20,10 @@
 //   waves 0..na-1  target actor j -> Gumbel a~_j                 | B2
 //   wave 3         critic forward L1, L2                        | B2 | head q | B3
 //   waves 4..7     target-critic L1 column tile on obs' | B2 | + a~ part | B3 | L2 tile | B4
-//                  wave 4: head q', fp64 TD, dL/dq, d2, dW3, db3 | B5
-//   waves 0..3     dh1 tile = (d2 W2^T) o [h1 > 0]  ||  waves 4..7 dW2, db2 | B6
-//   all            dW1, db1
+//                  wave 4: head q', fp64 TD, dL/dq (-> LDS flag), d2, dW3, db3 | B5
+//   waves 0..3     v = W3 o [h2 > 0] rows | B3 | u tile = (v W2^T) o [h1 > 0] | B4 |
+//                  wait for dq, dh1 tile = dq o u | B5   (the backward is linear in dq)
+//   all            dW2, db2, dW1, db1 (one phase)
 // k_actor_grad_r (maddpg.py:37-58):
 //   wave 0  actor forward, Gumbel a_i                              | B2
 //   waves 1..3  critic L1 on the replay part (a_i rows masked), one third of
@@ -31,7 +32,7 @@
 //   waves 0..3  one 16-column tile each of critic L2, d2c, q partials | B3
 //   waves 4..7  dh1c tiles                                         | B4
 //   wave 0  da = dh1c W1c[a_i]^T, softmax backward + reg -> dlogits, d2a, dW3a, db3a | B5
-//   waves 0..3 dW2a, db2a  ||  waves 4..7 dh1a tiles               | B6
+//   waves 0..3 dW2a (four tiles each, interleaved), db2a  ||  waves 4..7 dh1a tiles | B6
 //   all     dW1a, db1a
 #include "mdp_device.h"
 #include "mdp_kernels.h"
