@@ -293,7 +293,8 @@ inline bool grads_r_ok(const Topo& t, int agent) {
 }
 inline int lds_rollout_bytes(const Topo& t) {
   const int R = 16, ldr = mdp_ld(t.row_stride), ldh = t.H + 1;
-  return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8) + 2 * mdp_r4(R * 2 * MDP_MAX_ENT) +
+  const int par = t.H == 64 ? 4 * (2 * R * 68 + R * 8) : 0;  // k_rollout's per-agent forward slots (H = 64)
+  return 4 * (mdp_r4(R * ldr) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8) + par + 2 * mdp_r4(R * 2 * MDP_MAX_ENT) +
               mdp_r4(R * 3 * MDP_MAX_ENT) + mdp_r4(R * MDP_MAX_AGENTS) + mdp_r4(R));
 }
 inline int lds_eval_bytes(int in, int H) {

@@ -764,6 +764,9 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   float* h1 = cv.take(MDP_R * ldh);
   float* h2 = cv.take(MDP_R * ldh);
   float* lg = cv.take(MDP_R * 8);
+  // H = 64: every agent's policy forward on its own wave (rollout_par), h1 | h2 | logits per agent
+  constexpr int PAR_W = H == 64 ? MDP_NW * (2 * MDP_R * MDP_RLH + MDP_R * 8) : 0;
+  float* hpar = cv.take(PAR_W);
   float* sp = cv.take(MDP_R * 2 * MDP_MAX_ENT);
   float* sv = cv.take(MDP_R * 2 * MDP_MAX_ENT);
   float* sfo = cv.take(MDP_R * 3 * MDP_MAX_ENT);  // per-env force scratch of env_physics
@@ -846,8 +849,72 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   __syncthreads();
 
   MDP_STAMP(41);
-  // policies: act_j = gumbel_softmax(actor_j(obs_j))  (MADDPGAgentTrainer.action)
-  for (int j = 0; j < n; ++j) {
+  // policies: act_j = gumbel_softmax(actor_j(obs_j))  (MADDPGAgentTrainer.action).
+  // H = 64, n <= 4 agents: wave j runs agent j's whole forward from registers
+  // (all its fragments requested at once, the register kernels' one-wave net),
+  // the agents in parallel -- one after another over all four waves they took
+  // ~3 us each (stamped); the same MFMA k order per output, so the same values
+  bool par = false;
+  if constexpr (H == 64) {
+    par = !a.act_in && n <= MDP_NW;
+    for (int j = 0; j < n; ++j) par = par && T.ag[j].obs_dim <= 64;
+  }
+  if (par) {
+    if constexpr (H == 64) {
+      const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, r = lane & 15, kq = lane >> 4;
+      if (wave < n) {
+        const int j = wave;
+        const ADesc& aj = T.ag[j];
+        const NDesc& an = aj.actor;
+        const float* P = a.theta;
+        f32x4 w1[16], w2[16];
+        float w3[16];
+        rf_load<16>(w1, P + an.t[0].off, aj.obs_dim);
+        rf_load<16>(w2, P + an.t[2].off, MDP_RH);
+        rh_load(w3, P + an.t[4].off, MDP_ACT_DIM);
+        const f32x4 b1 = ld4(P + an.t[1].off + 4 * r), b2 = ld4(P + an.t[3].off + 4 * r);
+        const float b3 = P[an.t[5].off + min(r, MDP_ACT_DIM - 1)];
+        float u[MDP_ACT_DIM];  // the sample's uniforms, while the weights are in flight
+        if (lane < MDP_R) {
+          if (a.u_in) {
+            for (int k = 0; k < MDP_ACT_DIM; ++k)
+              u[k] = lane < nvalid ? a.u_in[((int64_t)(e0 + lane) * n + j) * MDP_ACT_DIM + k] : 0.5f;
+          } else {
+            uniforms5(a.seed, 0x10000u | (uint32_t)j, ctr_use(step_raw), (uint32_t)(a.env_base + e0 + lane), u);
+          }
+        }
+        float* h1j = hpar + j * (2 * MDP_R * MDP_RLH + MDP_R * 8);
+        float* h2j = h1j + MDP_R * MDP_RLH;
+        float* lgj = h2j + MDP_R * MDP_RLH;
+        {
+          f32x4 acc[4];
+          rf_zero(acc);
+          rf_acc<16>(acc, rowt + aj.obs_off, ldr, aj.obs_dim, w1);
+          rf_store<true>(acc, b1, h1j, MDP_RLH);
+        }
+        wave_sync();
+        {
+          f32x4 acc[4];
+          rf_zero(acc);
+          rf_acc<16>(acc, h1j, MDP_RLH, MDP_RH, w2);
+          rf_store<true>(acc, b2, h2j, MDP_RLH);
+        }
+        wave_sync();
+        {
+          const f32x4 acc = rh_acc(h2j, MDP_RLH, w3);
+          if (r < MDP_ACT_DIM) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lgj[(kq * 4 + i) * 8 + r] = acc[i] + b3;
+          }
+        }
+        wave_sync();
+        if (lane < MDP_R) gumbel_softmax5(lgj + lane * 8, u, rowt + lane * ldr + aj.act_off);
+      }
+      __syncthreads();
+      MDP_STAMP(42);
+    }
+  }
+  for (int j = 0; j < (par ? 0 : n); ++j) {
     const ADesc& aj = T.ag[j];
     if (!a.act_in) {
       bool pf = false;
