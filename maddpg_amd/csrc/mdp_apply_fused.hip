@@ -300,6 +300,17 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       }
       ss = wave_sum_d(ss);
       MDP_STAMP(35);
+      // the norm handshake's publish goes out first (its round trip is the
+      // launch's longest wait), the reduced-gradient stores behind it
+      uint64_t* part = f.sync_part + (int64_t)t * MDP_RA_MAXCH * 2;
+      const uint64_t tag = (uint64_t)nep << 32;
+      if (f.phase != 1 && nch > 1 && lane == 0) {
+        // this chunk's fp64 sum of squares as two epoch-tagged 64-bit words
+        // (high and low half) -- data and flag in one store, no counter RMW
+        const uint64_t bits = (uint64_t)__double_as_longlong(ss);
+        st_agent64(part + 2 * c, tag | (bits >> 32));
+        st_agent64(part + 2 * c + 1, tag | (bits & 0xffffffffull));
+      }
       if (act && f.phase != 2) {
         if (p0 + 3 < n) {
           *reinterpret_cast<f32x4*>(a.grad + i0) = g;
@@ -313,17 +324,8 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       double tot = ss;
       if (f.phase != 1) {  // phase 1 (data parallel) stops here: the all-reduce follows
       if (nch > 1) {
-        // publish this chunk's fp64 sum of squares as two epoch-tagged 64-bit
-        // words (high and low half) -- data and flag in one store, no counter
-        // RMW -- and read every chunk's pair back once both tags carry this
-        // step's epoch (bounded spin -> Ctl::fault = 1)
-        uint64_t* part = f.sync_part + (int64_t)t * MDP_RA_MAXCH * 2;
-        const uint64_t tag = (uint64_t)nep << 32;
-        if (lane == 0) {
-          const uint64_t bits = (uint64_t)__double_as_longlong(ss);
-          st_agent64(part + 2 * c, tag | (bits >> 32));
-          st_agent64(part + 2 * c + 1, tag | (bits & 0xffffffffull));
-        }
+        // read every chunk's pair (published above) back once both tags carry
+        // this step's epoch (bounded spin -> Ctl::fault = 1)
         MDP_STAMP(32);
         tot = 0.0;
         for (int q = lane; q < nch; q += 64) {
