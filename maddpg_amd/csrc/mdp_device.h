@@ -82,7 +82,24 @@ struct MdpTl {
 };
 #define MDP_TL(ctl, kind, role) MdpTl mdp_tl_(&(ctl)->upd_ctr, kind, role)
 #define MDP_TL_ROLE(kind, role) mdp_tl_.set_role(kind, role)
+// the last rollout launch's per-workgroup start / end (k_rollout, mdp_kernels.hip)
+__device__ unsigned long long g_mdp_tl_roll[MDP_TL_WG][2];
+struct MdpTlRoll {
+  unsigned long long t0;
+  __device__ MdpTlRoll() : t0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ ~MdpTlRoll() {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x < MDP_TL_WG) {
+      if (threadIdx.x == 0) g_mdp_tl_roll[blockIdx.x][0] = t0;
+      if ((threadIdx.x & 63) == 0) atomicMax(&g_mdp_tl_roll[blockIdx.x][1], t1);
+    }
+  }
+};
+#define MDP_TL_ROLLOUT() MdpTlRoll mdp_tlr_
 #else
+#define MDP_TL_ROLLOUT() \
+  do {                   \
+  } while (0)
 #define MDP_TL(ctl, kind, role) \
   do {                          \
   } while (0)

@@ -755,6 +755,7 @@ __device__ __forceinline__ void rollout_finish(const RolloutArgs& a, int64_t nex
 template <int H>
 __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  MDP_TL_ROLLOUT();
   const Topo& T = a.topo;
   const EnvDesc& E = a.env;
   const int n = E.n_agents, ne = E.n_agents + E.n_landmarks;
@@ -1184,6 +1185,19 @@ hipError_t mdp_launch_set_ring(Ctl* ctl, int64_t len, int64_t next, hipStream_t 
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
+
+#ifdef MDP_TIMELINE
+// diagnostic build: the last rollout's per-workgroup start / end (tools/step_boundary.py)
+extern "C" int mdp_debug_tl_roll(unsigned long long* out, int reset) {
+  const size_t n = sizeof(unsigned long long) * MDP_TL_WG * 2;
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_mdp_tl_roll)) != hipSuccess) return -1;
+    return hipMemset(p, 0, n) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_tl_roll), n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef MDP_STAMPS
 // diagnostic build: stamps of this translation unit's kernels (k_rollout: 40..47)
