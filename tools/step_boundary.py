@@ -6,7 +6,7 @@ host issues a step in ~0.05 ms of the ~0.93 ms it runs (tools/graph_gap_exp.py),
 so the host is not behind.
 
     make -C maddpg_amd/csrc timeline
-    MDP_LIB=maddpg_amd/libmaddpg_hip_tl.so [MDP_SB_EAGER=1] python tools/step_boundary.py
+    MDP_LIB=maddpg_amd/libmaddpg_hip_tl.so [MDP_SB_EAGER=1] [MDP_TL_CFG=tag6] python tools/step_boundary.py
 
 Per boundary: last optimizer end -> rollout first workgroup start, the
 rollout's body (first start -> last end), and rollout end -> first critic
@@ -37,15 +37,18 @@ def read(name, shape):
     return buf.reshape(shape)
 
 
-r = VecRunner("simple_spread", 1024, batch_size=1024, seed=0)
+if os.environ.get("MDP_TL_CFG") == "tag6":  # S5: only the rollout's own workgroups
+    r = VecRunner("simple_tag", 4096, n_agents=6, scenario_adversaries=4, batch_size=4096, num_units=128, seed=0)
+else:
+    r = VecRunner("simple_spread", 1024, batch_size=1024, seed=0)
 if os.environ.get("MDP_SB_EAGER") == "1":  # eager launches instead of the step graph
     r.eng.set_graphs(False)
 r.prefill()
 for _ in range(3):
     r.step()
 r.synchronize()
-pre, roll, post, rbody = [], [], [], []
-for rep in range(12):
+pre, roll, post, rbody, wg0, envmax, envmed, envst = [], [], [], [], [], [], [], []
+for rep in range(12 if os.environ.get("MDP_TL_CFG") != "tag6" else 4):
     for f in fns.values():
         assert f(None, 1) == 0
     k1 = r.step()
@@ -67,12 +70,20 @@ for rep in range(12):
     starts = np.concatenate(starts).astype(np.int64)
     before = ends[ends < rs]
     after = starts[starts > re_]
-    if len(before) == 0 or len(after) == 0:
-        continue
-    pre.append((rs - before.max()) / 100.0)
     rbody.append((re_ - rs) / 100.0)
-    post.append((after.min() - re_) / 100.0)
+    # workgroup 0 draws the first round's indices; the others step the env copies
+    wg0.append((int(ro[0, 1]) - rs) / 100.0)
+    envmax.append((int(ro[1:][ok[1:], 1].max()) - rs) / 100.0)
+    envmed.append((float(np.median(ro[1:][ok[1:], 1].astype(np.int64))) - rs) / 100.0)
+    envst.append((int(ro[1:][ok[1:], 0].max()) - rs) / 100.0)
+    if len(before) and len(after):  # instrumented launches on both sides (S2)
+        pre.append((rs - before.max()) / 100.0)
+        post.append((after.min() - re_) / 100.0)
 for nm, v in (("last optimizer end -> rollout start", pre), ("rollout body", rbody),
-              ("rollout end -> critic launch start", post)):
+              ("rollout end -> critic launch start", post), ("draw workgroup (0) end", wg0),
+              ("env workgroups: last start", envst), ("env workgroups: median end", envmed),
+              ("env workgroups: last end", envmax)):
     v = np.array(v)
+    if len(v) == 0:
+        continue
     print(f"{nm:>36s}: n={len(v):2d} median {np.median(v):6.2f} us (min {v.min():.2f}, max {v.max():.2f})")
