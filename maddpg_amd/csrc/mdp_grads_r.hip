@@ -43,6 +43,12 @@
 #ifdef MDP_STAMPS
 __device__ unsigned long long g_wg_t0[2][512];
 __device__ unsigned long long g_wg_t1[2][512][8];
+// critic_pre's per-wave phase points (row tile < 64, wave, point)
+__device__ unsigned long long g_cpre_t[64][8][6];
+#define CPRE_T(i)                                                                                   \
+  do {                                                                                              \
+    if ((threadIdx.x & 63) == 0 && bx < 64) g_cpre_t[bx][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define MDP_WG_START(k)                                                               \
   do {                                                                                \
     if (threadIdx.x == 0 && blockIdx.x < 512) g_wg_t0[k][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
@@ -58,6 +64,9 @@ __device__ unsigned long long g_wg_t1[2][512][8];
   } while (0)
 #define MDP_WG_END(k) \
   do {                \
+  } while (0)
+#define CPRE_T(i) \
+  do {            \
   } while (0)
 #endif
 
@@ -229,12 +238,14 @@ __device__ __forceinline__ void actor_pre_tile(const CriticArgs& a, float* lds, 
     *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(apre_lds(q, h1a, h2a, lg, av));
   store_rows16(rowbuf, ldr, T.row_stride, a.apre_rows + (int64_t)r0 * T.row_stride);
 }
-// float4 q of a row block [16][MDP_CPRE_W] <-> its LDS home (h1c | h2c | tacc | q + pad | a~ [16])
-__device__ __forceinline__ float* cpre_lds(int q, float* h1c, float* h2c, float* tacc, float* qv4, float* xa16) {
-  const int row = q / (MDP_CPRE_W / 4), c = 4 * (q - row * (MDP_CPRE_W / 4));
-  return c < 64 ? h1c + row * LH + c : c < 128 ? h2c + row * LH + c - 64 : c < 192 ? tacc + row * LH + c - 128
-                                                                         : c < 196 ? qv4 + row * 4
-                                                                                   : xa16 + row * 16 + c - 196;
+// one wave stores 16 rows x ncols (a multiple of 4) of an LDS tile into the
+// row block dst [16][MDP_CPRE_W] at column c0
+__device__ __forceinline__ void wave_store_cols16(const float* src, int ld, float* dst, int c0, int ncols) {
+  const int lane = threadIdx.x & 63, n4 = ncols >> 2;
+  for (int e = lane; e < MDP_R * n4; e += 64) {
+    const int r = e / n4, c = 4 * (e - r * n4);
+    *reinterpret_cast<f32x4*>(dst + r * MDP_CPRE_W + c0 + c) = *reinterpret_cast<const f32x4*>(src + r * ld + c);
+  }
 }
 // first MFMA k-step (of 4 inputs) of the target critic's a~ part that holds a
 // target action of agent p (columns 5 p .. 5 p + 4)
@@ -264,17 +275,19 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
   float* h2a = cv.take(3 * MDP_R * LH);
   float* h1c = cv.take(MDP_R * LH);
   float* h2c = cv.take(MDP_R * LH);
-  float* tacc = cv.take(MDP_R * LH);
-  float* qv4 = cv.take(MDP_R * 4);
-  float* xa16 = cv.take(MDP_R * 16);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane & 15, kq = lane >> 4;
   const int r0 = bx * MDP_R, nvalid = min(MDP_R, a.B - r0);
+  // the cpre block [16][MDP_CPRE_W]: h1c | h2c | target-critic accumulator |
+  // q + pad | a~ [16]; after B2 every wave stores its own part (no second
+  // barrier and workgroup-wide copy: that tail was ~1.7 µs of ~7 µs)
+  float* dst = a.cpre + (int64_t)r0 * MDP_CPRE_W;
   const uint32_t ctr = ctr_load(a.ctl) + 1u;  // critic k runs after p's actor step advanced the counter
   const float* Pc = a.theta;
   const float* Pt = a.target;
   if (threadIdx.x == 0) *rows_ready = 0;
   __syncthreads();
+  CPRE_T(0);
   if (wave < 3) {
     if (wave < na && wave != p) {
       const int j = wave;
@@ -294,6 +307,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
         gumbel_noise5(u, gn);
       }
       lds_wait(rows_ready, 4);
+      CPRE_T(1);
       float* h1 = h1a + wave * MDP_R * LH;
       float* h2 = h2a + wave * MDP_R * LH;
       float* lgj = lg + wave * MDP_R * 8;
@@ -327,7 +341,19 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
     } else if (wave == p && lane < MDP_R) {  // p's slot: zero weights meet zeros (not stale LDS, e.g. NaN)
       for (int q = 0; q < MDP_ACT_DIM; ++q) xa[lane * ldA + MDP_ACT_DIM * p + q] = 0.f;
     }
+    CPRE_T(2);
     __syncthreads();  // B2: a~_j (j != p) ready
+    CPRE_T(3);
+    // the gathered rows -> cpre_rows, by the three target-actor waves
+    {
+      const int v4 = T.row_stride >> 2;
+      float* rb = a.cpre_rows + (int64_t)r0 * T.row_stride;
+      for (int e = threadIdx.x; e < MDP_R * v4; e += 3 * 64) {
+        const int rr = e / v4, c4 = e - rr * v4;
+        const float* sp = rowbuf + rr * ldr + c4 * 4;
+        *reinterpret_cast<float4*>(rb + (int64_t)rr * T.row_stride + c4 * 4) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+      }
+    }
   } else if (wave == 3) {
     f32x4 w1[20], w2[16];
     float w3[16];
@@ -337,6 +363,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
     const f32x4 b1 = ld4(Pc + nd.t[1].off + 4 * r), b2 = ld4(Pc + nd.t[3].off + 4 * r);
     const float b3 = Pc[nd.t[5].off];
     lds_wait(rows_ready, 4);
+    CPRE_T(1);
     {
       f32x4 acc[4];
       rf_zero(acc);
@@ -352,11 +379,12 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
     }
     wave_sync();
     const float q = rq_head(h2c, LH, w3) + b3;
-    if ((lane & 3) == 0) {
-      qv4[(lane >> 2) * 4] = q;
-      qv4[(lane >> 2) * 4 + 1] = qv4[(lane >> 2) * 4 + 2] = qv4[(lane >> 2) * 4 + 3] = 0.f;
-    }
+    CPRE_T(2);
     __syncthreads();  // B2
+    CPRE_T(3);
+    wave_store_cols16(h1c, LH, dst, 0, RH);
+    wave_store_cols16(h2c, LH, dst, RH, RH);
+    if ((lane & 3) == 0) *reinterpret_cast<f32x4*>(dst + (lane >> 2) * MDP_CPRE_W + 3 * RH) = f32x4{q, 0.f, 0.f, 0.f};
   } else {
     const int tt = wave - 4, col = 16 * tt + r;
     gather_rows16_part(a.replay, T.row_stride, a.cpre_idx, r0, nvalid, rowbuf, ldr, 256, 256);
@@ -367,21 +395,23 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
     rt_load<16>(wa, Pt + nd.t[0].off, RH, col, ka_t);
     rt_load_k<5>(wb, Pt + nd.t[0].off + ka_t * RH, RH, col, 4 * ks);
     lds_wait(rows_ready, 4);
+    CPRE_T(1);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     rt_acc<16>(acc, rowbuf + xo_t, ldr, ka_t, wa);
+    CPRE_T(2);
     __syncthreads();  // B2: a~ ready
+    CPRE_T(3);
+    // every a~_j (p's slot zero: the critic step writes it), one per lane of waves 4..7
+    {
+      const int e = 64 * tt + lane, rr = e >> 4, c = e & 15;
+      dst[rr * MDP_CPRE_W + 3 * RH + 4 + c] = c < kb ? xa[rr * ldA + c] : 0.f;
+    }
     if (ks > 0) rt_acc<5>(acc, xa, ldA, 4 * ks, wb);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tacc[(kq * 4 + i) * LH + col] = acc[i];
-    if (tt == 0 && lane < MDP_R) {  // every a~_j (p's slot zero: the critic step writes it)
-      for (int c = 0; c < 16; ++c) xa16[lane * 16 + c] = c < kb ? xa[lane * ldA + c] : 0.f;
-    }
+    for (int i = 0; i < 4; ++i) dst[(kq * 4 + i) * MDP_CPRE_W + 2 * RH + col] = acc[i];
+    CPRE_T(4);
   }
-  __syncthreads();  // B3
-  float* dst = a.cpre + (int64_t)r0 * MDP_CPRE_W;
-  for (int q = threadIdx.x; q < MDP_R * MDP_CPRE_W / 4; q += blockDim.x)
-    *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(cpre_lds(q, h1c, h2c, tacc, qv4, xa16));
-  store_rows16(rowbuf, ldr, T.row_stride, a.cpre_rows + (int64_t)r0 * T.row_stride);
+  CPRE_T(5);
 }
 }  // namespace
 
@@ -1126,6 +1156,10 @@ extern "C" int mdp_debug_tl_r(unsigned long long* out, int reset) {
 // diagnostic build: stamps of this translation unit's kernels (own code object)
 extern "C" int mdp_debug_stamps_r(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+// critic_pre's per-wave phase points [64][8][6] (CPRE_T)
+extern "C" int mdp_debug_cpre_times(unsigned long long* t) {
+  return hipMemcpyFromSymbol(t, HIP_SYMBOL(g_cpre_t), sizeof(unsigned long long) * 64 * 8 * 6) == hipSuccess ? 0 : -1;
 }
 // [2][512] starts, then [2][512][8] per-wave ends
 extern "C" int mdp_debug_wg_times(unsigned long long* t0, unsigned long long* t1) {

@@ -4,7 +4,8 @@
     MDP_LIB=maddpg_amd/libmaddpg_hip_stamps.so python tools/wg_times.py
 Per role of the last k_critic_grad_r / k_actor_grad_r launch of a round:
 the earliest start, the latest start and the latest end, in us after the
-launch's first workgroup started (s_memrealtime, 100 MHz)."""
+launch's first workgroup started (s_memrealtime, 100 MHz), and each wave's
+end after its own workgroup's start."""
 import ctypes
 import os
 import sys
@@ -45,3 +46,27 @@ for k, name, roles in ((0, "critic launch", [("critic step", 0, nwg), ("actor_pr
         e = t1[k][lo:hi].max(axis=1)
         print(f"  {rn:>12s}: start {(s.min() - base) / 100:5.2f}..{(s.max() - base) / 100:5.2f} us, "
               f"end median {(np.median(e) - base) / 100:5.2f}, max {(e.max() - base) / 100:5.2f} us")
+        # per wave: end after its own workgroup's start (median over the role's workgroups)
+        ok = s > 0
+        w = t1[k][lo:hi][ok]
+        rel = np.where(w > 0, w - s[ok][:, None], -1)
+        print(" " * 16 + "per-wave end after own start (us): " +
+              " ".join(f"w{q}:{np.median(rel[:, q]) / 100:.2f}" if (rel[:, q] >= 0).any() else f"w{q}:-"
+                       for q in range(8)))
+
+# critic_pre's per-wave phase points (us after the workgroup's first point,
+# median over its row tiles): 1 rows ready, 2 at B2, 3 after B2, 4 stores issued (waves 4..7), 5 end
+f2 = lib.mdp_debug_cpre_times
+f2.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+ct = (ctypes.c_ulonglong * (64 * 8 * 6))()
+assert f2(ct) == 0
+ct = np.array(ct[:], dtype=np.int64).reshape(64, 8, 6)
+base = ct[:, :, 0].min(axis=1)
+print("critic_pre phase points (us after the tile's start; waves 0..2 target actors, 3 critic, 4..7 gather + target-critic tiles)")
+for q in range(8):
+    row = []
+    for i in range(1, 6):
+        v = ct[:, q, i]
+        ok = v > 0
+        row.append(f"{np.median(v[ok] - base[ok]) / 100:5.2f}" if ok.any() else "    -")
+    print(f"  w{q}: rows {row[0]}  B2 {row[1]} -> {row[2]}  stores {row[3]}  end {row[4]}")
