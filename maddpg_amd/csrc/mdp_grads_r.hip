@@ -45,6 +45,12 @@ __device__ unsigned long long g_wg_t0[2][512];
 __device__ unsigned long long g_wg_t1[2][512][8];
 // critic_pre's per-wave phase points (row tile < 64, wave, point)
 __device__ unsigned long long g_cpre_t[64][8][6];
+// the critic step's per-wave points after B5 (row tile < 64, wave, point)
+__device__ unsigned long long g_crit_t[64][8][6];
+#define CRIT_T(i)                                                                                   \
+  do {                                                                                              \
+    if ((threadIdx.x & 63) == 0 && bx < 64) g_crit_t[bx][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define CPRE_T(i)                                                                                   \
   do {                                                                                              \
     if ((threadIdx.x & 63) == 0 && bx < 64) g_cpre_t[bx][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memrealtime(); \
@@ -66,6 +72,9 @@ __device__ unsigned long long g_cpre_t[64][8][6];
   do {                \
   } while (0)
 #define CPRE_T(i) \
+  do {            \
+  } while (0)
+#define CRIT_T(i) \
   do {            \
   } while (0)
 #endif
@@ -859,12 +868,17 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   // interleaved, stores last -- measured slower: S2 1.074M -> 1.048M with all
   // five tiles of a wave at once, 1.064M as 2 + 3: the stores of the first
   // tiles no longer drain behind the later tiles' work)
+  CRIT_T(0);
   wgrad_waves(h1c, LH, RH, d2, LD, RH, slab + nd.t[2].off, 0, 8);
+  CRIT_T(1);
   wgrad_waves(rowbuf + xo_c, ldr, ka_c, d1, LD, RH, slab + nd.t[0].off, 0, 8);
+  CRIT_T(2);
   if (kb_c) wgrad_waves(rowbuf + ag.act_off, ldr, kb_c, d1, LD, RH, slab + nd.t[0].off + ka_c * RH, 0, 8);
+  CRIT_T(3);
   if (wave == 4) MDP_STAMPW(9);
   if (wave == 5) colsum64(d2, LD, slab + nd.t[3].off);
   if (wave == 7) colsum64(d1, LD, slab + nd.t[1].off);
+  CRIT_T(4);
   MDP_STAMP(10);
   MDP_WG_END(0);
 }
@@ -1156,6 +1170,10 @@ extern "C" int mdp_debug_tl_r(unsigned long long* out, int reset) {
 // diagnostic build: stamps of this translation unit's kernels (own code object)
 extern "C" int mdp_debug_stamps_r(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+// the critic step's per-wave points after B5 [64][8][6] (CRIT_T)
+extern "C" int mdp_debug_crit_times(unsigned long long* t) {
+  return hipMemcpyFromSymbol(t, HIP_SYMBOL(g_crit_t), sizeof(unsigned long long) * 64 * 8 * 6) == hipSuccess ? 0 : -1;
 }
 // critic_pre's per-wave phase points [64][8][6] (CPRE_T)
 extern "C" int mdp_debug_cpre_times(unsigned long long* t) {

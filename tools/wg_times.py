@@ -70,3 +70,16 @@ for q in range(8):
         ok = v > 0
         row.append(f"{np.median(v[ok] - base[ok]) / 100:5.2f}" if ok.any() else "    -")
     print(f"  w{q}: rows {row[0]}  B2 {row[1]} -> {row[2]}  stores {row[3]}  end {row[4]}")
+
+# the critic step after B5 (weight-gradient tiles, column sums), per wave: us
+# after the workgroup's earliest B5 exit, median over its row tiles
+f3 = lib.mdp_debug_crit_times
+f3.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+ct = (ctypes.c_ulonglong * (64 * 8 * 6))()
+assert f3(ct) == 0
+ct = np.array(ct[:], dtype=np.int64).reshape(64, 8, 6)
+base = ct[:, :, 0].min(axis=1)
+print("critic step after B5 (us after the tile's first B5 exit)")
+for q in range(8):
+    row = [f"{np.median(ct[:, q, i] - base) / 100:5.2f}" for i in range(5)]
+    print(f"  w{q}: B5 exit {row[0]}  dW2 {row[1]}  dW1 obs {row[2]}  dW1 act {row[3]}  colsums {row[4]}")
