@@ -950,6 +950,8 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   if (threadIdx.x == 1) fwd_issued = 0;
   __syncthreads();  // B0
 
+  // wave 0's loss / stat terms (rows = lanes 0..15), summed at the end, off the path to B4b
+  double s_q = 0.0, s_p = 0.0;
   if (wave < 4) {
     if (wave == 0) {
       // ---------------- actor forward on obs_i -> logits p (maddpg.py:39), sample a_i (:49)
@@ -1005,8 +1007,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
         }
       }
       wave_sync();
-      // softmax backward + regulariser: dlogits = (da - sum(a da)) a + reg 2 p / (B A); loss partials
-      double s_q = 0.0, s_p = 0.0;
+      // softmax backward + regulariser: dlogits = (da - sum(a da)) a + reg 2 p / (B A); loss terms
       if (lane < MDP_R) {
         float dot = 0.f;
         for (int k = 0; k < MDP_ACT_DIM; ++k) dot += da[lane * 8 + k] * av[lane * 8 + k];
@@ -1021,13 +1022,6 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
             s_p += p * p;
           }
         }
-      }
-      s_q = sum16(s_q);
-      s_p = sum16(s_p);
-      if (lane == 0) {
-        double* st = slab_stat + (int64_t)bx * 8;
-        st[0] = s_q;
-        st[1] = s_p;
       }
       __syncthreads();  // B4b: dlogits ready
       d2a_rows(h2a, dl, w3a, d2a, gwpart, 0);
@@ -1124,6 +1118,15 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   // dW1a = obs_i^T dh1a over all waves, db1a
   wgrad_waves(rowbuf + ag.obs_off, ldr, ag.obs_dim, d1a, LD, RH, slab + na.t[0].off, 0, 8);
   if (wave == 7) colsum64(d1a, LD, slab + na.t[1].off);
+  if (wave == 0) {  // the update's stats: this tile's partial sums
+    s_q = sum16(s_q);
+    s_p = sum16(s_p);
+    if (lane == 0) {
+      double* st = slab_stat + (int64_t)bx * 8;
+      st[0] = s_q;
+      st[1] = s_p;
+    }
+  }
   MDP_STAMP(27);
   MDP_WG_END(1);
 }
