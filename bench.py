@@ -30,6 +30,7 @@ from maddpg_amd import _lib  # noqa: E402
 from maddpg_amd.parallel import init_process_group_from_env  # noqa: E402
 from maddpg_amd.runner import VecRunner  # noqa: E402
 
+MARKER_KINDS = ("allreduce", "gather")   # timed by marker events around the call (mdp_api.cpp ProfScope)
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix/vector dense peak
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 
@@ -55,6 +56,34 @@ def flops_actor_grad(eng, agent):
     return 2.0 * B * mac
 
 
+def bytes_critic_grad(eng, agent):
+    """algorithmic bytes of one agent's critic step: the B fused replay
+    rows (every agent's obs, act, obs', rew, done) + the indices + 8 touches of the
+    critic (theta, target, Adam m/v read and written, grad) + every target actor read"""
+    B, o, n = eng.batch_size, eng.obs_dims, eng.n
+    row = 4 * (2 * sum(o) + 5 * n + 2)
+    actors = [agent] if eng.local_q[agent] else range(n)
+    return B * row + 4 * B + 4 * (8 * param_count(eng, agent, "critic") +
+                                  sum(param_count(eng, j, "actor") for j in actors))
+
+
+def bytes_actor_grad(eng, agent):
+    """algorithmic bytes of one agent's actor step: the critic-input rows, the
+    indices, the critic read once, 8 touches of the actor (theta, target, Adam)"""
+    B, o, n = eng.batch_size, eng.obs_dims, eng.n
+    cin = o[agent] + 5 if eng.local_q[agent] else sum(o) + 5 * n
+    return 4 * B * cin + 4 * B + 4 * (param_count(eng, agent, "critic") + 8 * param_count(eng, agent, "actor"))
+
+
+def param_count(eng, agent, net):
+    """logical parameter count of one net (maddpg.py:113-149, mlp_model train.py:39-46)"""
+    H, o, n = eng.num_units, eng.obs_dims, eng.n
+    if net == "actor":
+        return o[agent] * H + H + H * H + H + 5 * H + 5
+    cin = o[agent] + 5 if eng.local_q[agent] else sum(o) + 5 * n
+    return cin * H + H + H * H + H + H + 1
+
+
 def bytes_rollout(eng):
     ne = eng.n_entities
     per_env = 4 * eng.row_stride + 2 * 2 * (4 * 2 * ne) + 16 + 4 * eng.n
@@ -70,12 +99,13 @@ def roofline_for(kind, eng, ms_avg):
         # rides in the critic launch, the next critic step's independent part in
         # the actor launch), so the algorithmic flops are attributed to the pair
         fl = sum(flops_critic_grad(eng, i) + flops_actor_grad(eng, i) for i in range(eng.n)) / (1 if tp else eng.n)
+        by = sum(bytes_critic_grad(eng, i) + bytes_actor_grad(eng, i) for i in range(eng.n)) / (1 if tp else eng.n)
         ach = fl / (ms_avg * 1e-3) / 1e12
         return {"bound": "mfma", "achieved": round(ach, 4), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 6), "traffic": None,
                 "kernel": f"k_critic_grad{suffix}+k_actor_grad{suffix}", "kernels": [f"k_critic_grad{suffix}",
                                                                                f"k_actor_grad{suffix}"],
-                "algorithmic_per_launch": fl, "avg_launch_ms": ms_avg,
+                "algorithmic_per_launch": fl, "algorithmic_bytes_per_launch": by, "avg_launch_ms": ms_avg,
                 "launch_unit": "one critic-step launch + one actor-step launch (one agent's update)"}
     if kind in ("critic_grad", "actor_grad"):
         f = flops_critic_grad if kind == "critic_grad" else flops_actor_grad
@@ -256,6 +286,9 @@ def main():
                     help="skip the secondary throughput-mode measurement of a strict run")
     ap.add_argument("--no-configs2", action="store_true",
                     help="skip the 4096-envs-per-GPU figure (BASELINE configs[2]) of an N=1 run")
+    ap.add_argument("--allow-torch-dist", action="store_true",
+                    help="N>1: accept the torch.distributed fallback exchange (~14x slower per round) when "
+                         "neither the direct xGMI exchange nor the library's RCCL communicator came up")
     ap.add_argument("--no-gather-stage", action="store_true",
                     help="skip the gather-only stage figure (SURVEY 8d, rank 0 at N=1)")
     args = ap.parse_args()
@@ -272,6 +305,14 @@ def main():
                   num_units=args.num_units, seed=args.seed, train_every=args.train_every, world_size=world,
                   rank=rank)
     eng = r.eng
+    if (world > 1 and not r.native_dp and os.environ.get("MDP_NATIVE_DP", "1") == "1"
+            and not args.allow_torch_dist):
+        # the native exchanges (direct xGMI, then RCCL from C++) both failed to set up:
+        # a line measured on the host-driven fallback would misreport the path
+        print(f"rank {rank}: data-parallel exchange fell back to {r.dp_kind} (native xGMI and RCCL "
+              f"set-up failed); refusing to report it -- pass --allow-torch-dist to measure it anyway",
+              file=sys.stderr)
+        sys.exit(3)
     if args.update_mode != "strict":
         eng.set_update_mode(args.update_mode)
     r.prefill()
@@ -288,8 +329,6 @@ def main():
     r.synchronize()
 
     xgmi = world > 1 and getattr(r, "dp_kind", None) == "native-xgmi"
-    if xgmi:
-        eng.dp_exchange_stats(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -313,8 +352,6 @@ def main():
     r.synchronize()
     info = {"ms_per_step": round(dt_local / args.steps * 1e3, 4), "checksum": eng.param_checksum(),
             "rounds": rounds}
-    if xgmi:   # in-kernel stamps of the timed region's exchanges (graph replays)
-        info["xgmi_wait"] = eng.dp_exchange_stats(reset=True)
     if world > 1:
         info["dp"] = eng.dp_info() if getattr(r, "native_dp", False) else {"kind": r.dp_kind, "ranks": world}
         allinfo = [None] * world
@@ -348,10 +385,16 @@ def main():
     # eager launch path; the timed region above replays the captured round graph).
     for k in kinds:
         eng.prof_enable(k, True)
+    if xgmi:   # the exchange waits are stamped in this pass only (off in the timed graphs)
+        eng.dp_exchange_stats_enable(True)
+        eng.dp_exchange_stats(reset=True)
     prof_steps = max(3, args.steps // 3)
     for _ in range(prof_steps):
         one_step()
     r.synchronize()
+    if xgmi:
+        info["xgmi_wait"] = eng.dp_exchange_stats(reset=True)
+        eng.dp_exchange_stats_enable(False)
     per_kind = {k: eng.prof_read(k) for k in kinds}
     for k in kinds:
         eng.prof_enable(k, False)
@@ -366,7 +409,8 @@ def main():
               "round_us": round(round_us, 3) if round_us else None}
         if xgmi:
             w = info["xgmi_wait"]
-            ex.update(source="in-kernel s_memrealtime: chunk stores -> every peer's chunk arrived",
+            ex.update(source="in-kernel s_memrealtime in the eager kernel pass: chunk stores -> every "
+                             "peer's chunk arrived",
                       per_exchange_us=round(w["mean_us"], 3), longest_wait_us=round(w["max_us"], 3),
                       chunk_exchanges=w["chunk_exchanges"])
         elif per_kind.get("allreduce", (0, 0))[1]:
@@ -385,11 +429,11 @@ def main():
     if per_kind["critic_grad"][1] and per_kind["critic_grad"][1] == per_kind["actor_grad"][1]:
         per_kind["grads"] = (per_kind["critic_grad"][0] + per_kind["actor_grad"][0], per_kind["critic_grad"][1])
     modelled = [k for k in ("grads", "rollout", "reduce_apply") if per_kind.get(k, (0, 0))[1]]
-    ev_pre = event_overhead_ms(eng.stream)
-    # (a pair carries two event pairs' overhead per "launch")
-    evn = {"grads": 2}
-    dominant = max(modelled, key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_pre * evn.get(k, 1)) \
-        if modelled else None
+    # every kernel kind is timed on its own dispatch packet (hipExtLaunchKernel
+    # start/stop events: the packet's begin -> end, what rocprofv3 reports), so
+    # no marker overhead is subtracted; only the RCCL call and the multi-launch
+    # gather are bracketed by marker events (MARKER_KINDS)
+    dominant = max(modelled, key=lambda k: per_kind[k][0]) if modelled else None
     ms_tot, launches = per_kind[dominant] if dominant else (0.0, 0)
 
     # secondary figure: the same workload in throughput mode (every
@@ -435,13 +479,12 @@ def main():
     ev_ms = event_overhead_ms(eng.stream)
     roof = None
     if launches:
-        raw = ms_tot / launches
-        roof = roofline_for(dominant, eng, max(raw - ev_ms * evn.get(dominant, 1), 1e-6))
-        roof["dominant_of_all_kinds"] = max(
-            (k for k in per_kind if per_kind[k][1] and k != "grads"),
-            key=lambda k: per_kind[k][0] - per_kind[k][1] * ev_ms)
-        roof["avg_launch_ms_raw_events"] = raw
-        roof["event_pair_overhead_ms"] = ev_ms
+        roof = roofline_for(dominant, eng, ms_tot / launches)
+        roof["dominant_of_all_kinds"] = max((k for k in per_kind if per_kind[k][1] and k != "grads"),
+                                            key=lambda k: per_kind[k][0])
+        roof["timing"] = ("HIP start/stop events carried on each launch's own dispatch packet "
+                          "(hipExtLaunchKernel) in an eager pass of the same workload; the pair's two "
+                          "launch durations summed")
         roof["launches_timed"] = launches
     cfg_key = f"{args.scenario}_E{args.num_envs}_B{args.batch_size}_H{args.num_units}"
     if args.num_agents is not None:
@@ -465,11 +508,15 @@ def main():
             roof["mfma_busy_frac_rocprof"] = round(pmc["mfma_busy_frac"], 5)
         if pmc.get("avg_ns"):
             # the committed rocprofv3 --kernel-trace --stats average of the same kernel and
-            # workload: it spans dispatch to completion signal (incl. the ramp and the
-            # end-of-kernel release), the event figure above subtracts an empty pair's cost
+            # workload (profiles/): the live packet-event figure above must agree with it
             roof["rocprof_avg_launch_ms"] = round(pmc["avg_ns"] * 1e-6, 6)
             roof["frac_at_rocprof_duration"] = round(
                 roof["frac"] * roof["avg_launch_ms"] / roof["rocprof_avg_launch_ms"], 6)
+            roof["live_vs_rocprof_duration"] = round(roof["avg_launch_ms"] / roof["rocprof_avg_launch_ms"], 4)
+        if roof.get("traffic") and roof.get("algorithmic_bytes_per_launch"):
+            # counted HBM bytes (2*FETCH + WRITE) over the algorithmic bytes: the re-read /
+            # write-back excess of the launch (partial-gradient slabs, hand-off blocks, weights per XCD)
+            roof["traffic_ratio"] = round(roof["traffic"] / roof["algorithmic_bytes_per_launch"], 3)
         if pmc.get("_source") or pmc:
             roof["pmc_source"] = "profiles/pmc_traffic.json"
     if rank == 0:
@@ -501,8 +548,11 @@ def main():
             "update_rounds": rounds,
             "dp": r.dp_kind if world > 1 else None,
             "dp_check": dp_check,
-            "kernel_pass": {"steps": prof_steps, "event_pair_overhead_ms": round(ev_ms, 5),
-                            "per_kind_ms_per_launch": {k: round(v[0] / v[1] - ev_ms, 5) for k, v in per_kind.items()
+            "kernel_pass": {"steps": prof_steps, "marker_pair_overhead_ms": round(ev_ms, 5),
+                            "timing": "dispatch-packet events per launch; marker pairs (their overhead "
+                                      "subtracted) only for " + ", ".join(MARKER_KINDS),
+                            "per_kind_ms_per_launch": {k: round(v[0] / v[1] - (ev_ms if k in MARKER_KINDS else 0.0),
+                                                                5) for k, v in per_kind.items()
                                                        if v[1] and k != "grads"},
                             "per_kind_launches": {k: v[1] for k, v in per_kind.items() if k != "grads"}},
             "roofline": roof,

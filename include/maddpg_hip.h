@@ -215,6 +215,11 @@ int mdp_dp_info(mdp_handle* h, int32_t out4[4]);
  * since the last reset; reset != 0 zeroes the counters.  The RCCL path's cost
  * is event-timed instead (mdp_prof_enable(MDP_K_ALLREDUCE)). */
 int mdp_dp_exchange_stats(mdp_handle* h, double out4[4], int32_t reset);
+/* collect those stamps (on != 0) in the optimizer launches issued from now on
+ * while enabled -- eager launches and graphs captured meanwhile; graphs
+ * captured with it off carry no stamping code path (default off: the three
+ * counter atomics per chunk stay out of the exchange's critical path) */
+int mdp_dp_exchange_stats_enable(mdp_handle* h, int32_t on);
 /* Co-residency plan of the spin-waiting optimizer launch (k_reduce_apply: the
  * chunk workgroups of a tensor wait for each other's norm partials, the xGMI
  * exchange for the peers' chunks).  For cfg on a device with `cus` CUs that

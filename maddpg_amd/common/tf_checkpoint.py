@@ -195,7 +195,7 @@ def _parse_entry(buf):
                         if h == 1:
                             size = s
                     e["shape"].append(size)
-                elif g == 3 and v:
+                elif g == 3 and d:
                     raise ValueError("unknown-rank tensor in checkpoint")
         elif f == 3:
             e["shard_id"] = v

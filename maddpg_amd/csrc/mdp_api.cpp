@@ -339,6 +339,7 @@ struct mdp_handle {
   uint32_t* x_probe = nullptr;        // [0] mismatches, [1] fault of the connection probe
   uint32_t x_probe_ep = 0;
   bool p2p = false;
+  bool xw_stats = false;              // stamp the exchange waits (mdp_dp_exchange_stats_enable)
 };
 
 namespace {
@@ -360,12 +361,26 @@ int fail(mdp_handle* h, const char* what, hipError_t e = hipSuccess) {
     if (e__ != hipSuccess) return fail(h, #call, e__); \
   } while (0)
 
-// bracket one launch with timing events when profiling `kind`
+}  // namespace
+
+MdpLaunchEv& mdp_launch_ev() {
+  static thread_local MdpLaunchEv e;
+  return e;
+}
+
+namespace {
+
+// time one launch when profiling `kind`.  packet (the kernel launchers, which
+// go through mdp_launch): the pair rides on the launch's own dispatch packet,
+// so the elapsed time is that packet's begin -> end, the interval rocprofv3
+// reports.  Otherwise (an RCCL call, a multi-launch gather) the pair is
+// recorded as markers around the scope and includes their own cost.
 struct ProfScope {
   mdp_handle* h;
   int kind;
+  bool packet;
   hipEvent_t stop = nullptr;
-  ProfScope(mdp_handle* hh, int k) : h(hh), kind(k) {
+  ProfScope(mdp_handle* hh, int k, bool pk = true) : h(hh), kind(k), packet(pk) {
     if (!h->prof_on[kind] || h->capturing) return;
     auto& pool = h->ev[kind];
     size_t u = h->ev_used[kind];
@@ -376,12 +391,25 @@ struct ProfScope {
         pool.push_back(e);
       }
     }
-    (void)hipEventRecord(pool[u], h->stream);
-    stop = pool[u + 1];
     h->ev_used[kind] = u + 2;
+    stop = pool[u + 1];
+    if (packet) {
+      mdp_launch_ev() = MdpLaunchEv{pool[u], pool[u + 1]};
+    } else {
+      (void)hipEventRecord(pool[u], h->stream);
+    }
   }
   ~ProfScope() {
-    if (stop) (void)hipEventRecord(stop, h->stream);
+    if (!stop) return;
+    if (!packet) {
+      (void)hipEventRecord(stop, h->stream);
+      return;
+    }
+    MdpLaunchEv& e = mdp_launch_ev();
+    if (e.start) {  // nothing was launched (an error path): drop the unrecorded pair
+      e.start = e.stop = nullptr;
+      h->ev_used[kind] -= 2;
+    }
   }
 };
 
@@ -636,6 +664,7 @@ FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net, bool tp = false
   f.xd = nullptr;
   f.net_id = g;
   f.xstep = nullptr;
+  f.wstat = nullptr;
   f.pf_count = 0;
   f.pf_out = nullptr;
   f.pf_ctl = h->ctl;
@@ -649,6 +678,7 @@ void set_xchg(mdp_handle* h, FusedApplyArgs& f, int agent, int net) {
   f.xd = h->xd_dev;
   f.net_id = 2 * agent + net;
   f.xstep = h->ctl->xstep + f.net_id;
+  f.wstat = h->xw_stats ? &h->ctl->xw_ticks : nullptr;
 }
 
 void xgmi_release(mdp_handle* h) {
@@ -712,8 +742,16 @@ RcclApi& rccl() {
   static RcclApi r;
   if (!r.tried) {
     r.tried = true;
-    void* so = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!so) so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    // MDP_RCCL_LIB: another library with RCCL's entry points (the tests'
+    // one-GPU stand-in communicator, tests/rccl_standin/); no fallback then
+    const char* alt = getenv("MDP_RCCL_LIB");
+    void* so = nullptr;
+    if (alt && alt[0]) {
+      so = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      so = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+      if (!so) so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    }
     if (so) {
       r.get_id = (decltype(r.get_id))dlsym(so, "ncclGetUniqueId");
       r.init_rank = (decltype(r.init_rank))dlsym(so, "ncclCommInitRank");
@@ -731,7 +769,7 @@ RcclApi& rccl() {
 int dp_allreduce(mdp_handle* h, int agent, int net) {
   const NDesc& d = net_of(h, agent, net);
   float* g = h->grad + d.off;
-  ProfScope p(h, MDP_K_ALLREDUCE);
+  ProfScope p(h, MDP_K_ALLREDUCE, false);
   const ncclResult_t r = rccl().all_reduce(g, g, (size_t)d.size, ncclFloat32, ncclSum, h->comm, h->stream);
   if (r != ncclSuccess) {
     h->err = std::string("ncclAllReduce: ") + rccl().err(r);
@@ -742,7 +780,7 @@ int dp_allreduce(mdp_handle* h, int agent, int net) {
 
 // throughput mode: the whole grad region (every agent's actor + critic) in one call
 int dp_allreduce_all(mdp_handle* h) {
-  ProfScope p(h, MDP_K_ALLREDUCE);
+  ProfScope p(h, MDP_K_ALLREDUCE, false);
   const ncclResult_t r = rccl().all_reduce(h->grad, h->grad, (size_t)h->L.PT, ncclFloat32, ncclSum, h->comm, h->stream);
   if (r != ncclSuccess) {
     h->err = std::string("ncclAllReduce: ") + rccl().err(r);
@@ -778,22 +816,22 @@ struct DrawPieces {
   int n_critic = 0, n_actor = 0;
 };
 
-int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out, int post_prev, int pre_next,
-                 const int32_t* pre_idx, const DrawPieces& dp) {
+int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act,
+                 int32_t* pf_out, int post_prev, int pre_next, const int32_t* pre_idx, const DrawPieces& dp) {
   const float scale = 1.0f / (float)h->dp_world;
   const bool pre = actor_pre_ok(h, agent);
   int rc;
   if (h->p2p) {  // the exchange lives inside the optimizer launch: same 4 launches as one GPU
-    if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre, nullptr, post_prev))) return rc;
+    if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev))) return rc;
     if ((rc = do_reduce_apply(h, agent, 1, dp.out, dp.n_critic))) return rc;
-    if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre, pre_next, pre_idx))) return rc;
+    if ((rc = do_actor_grad(h, agent, idx, u_act, false, pre, pre_next, pre_idx))) return rc;
     return do_reduce_apply(h, agent, 0, dp.out ? dp.out + dp.n_critic : nullptr, dp.n_actor);
   }
-  if ((rc = do_critic_grad(h, agent, idx, nullptr, pf_out, false, pre, nullptr, post_prev))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev))) return rc;
   if ((rc = do_reduce(h, agent, 1))) return rc;
   if ((rc = dp_allreduce(h, agent, 1))) return rc;
   if ((rc = do_apply(h, agent, 1, false, scale))) return rc;
-  if ((rc = do_actor_grad(h, agent, idx, nullptr, false, pre, pre_next, pre_idx))) return rc;
+  if ((rc = do_actor_grad(h, agent, idx, u_act, false, pre, pre_next, pre_idx))) return rc;
   if ((rc = do_reduce(h, agent, 0))) return rc;
   if ((rc = dp_allreduce(h, agent, 0))) return rc;
   return do_apply(h, agent, 0, false, scale);
@@ -806,8 +844,9 @@ int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, int32_t* pf_out, 
 int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act,
               int32_t* pf_out = nullptr, int post_prev = -1, int pre_next = -1, const int32_t* pre_idx = nullptr,
               const DrawPieces& dp = DrawPieces()) {
-  if ((h->comm || h->p2p) && !u_tgt && !u_act)
-    return do_update_dp(h, agent, idx, pf_out, post_prev, pre_next, pre_idx, dp);
+  // data parallel: the exchange runs whatever the noise source (injected
+  // uniforms included -- an update that skipped it would split the replicas)
+  if (h->comm || h->p2p) return do_update_dp(h, agent, idx, u_tgt, u_act, pf_out, post_prev, pre_next, pre_idx, dp);
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
   const bool pre = actor_pre_ok(h, agent);
@@ -1013,21 +1052,21 @@ int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const flo
                             : tp_grads_general(h, idx, u_tgt, u_act, pf_out);
   if (rc) return rc;
   if (h->p2p) {  // data parallel over xGMI: reduce + exchange + step of every net, one launch
-    ProfScope p(h, MDP_K_REDUCE_APPLY);
+    ProfScope p(h, MDP_K_REDUCE_APPLY, h->tp_fits[3]);
     return launch_tp_batch(h, 3);
   }
   if (h->comm) {  // data parallel: ONE all-reduce of every net's gradient per round
     {
-      ProfScope p(h, MDP_K_REDUCE);
+      ProfScope p(h, MDP_K_REDUCE, h->tp_fits[1]);
       const int rc = launch_tp_batch(h, 1);
       if (rc) return rc;
     }
     const int rc = dp_allreduce_all(h);
     if (rc) return rc;
-    ProfScope p(h, MDP_K_APPLY);
+    ProfScope p(h, MDP_K_APPLY, h->tp_fits[2]);
     return launch_tp_batch(h, 2);
   }
-  ProfScope p(h, MDP_K_REDUCE_APPLY);
+  ProfScope p(h, MDP_K_REDUCE_APPLY, h->tp_fits[0]);
   return launch_tp_batch(h, 0);
 }
 
@@ -1105,6 +1144,12 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     HIPCHK(h, mdp_ra_batch_occupancy(&per_b));
     h->ra_cap = cus * per;
     h->ra_batch_cap = cus * per_b;
+    // a spinning grid with scratch may not be co-resident (scratch-slot
+    // throttling): no fused / exchanging launch then -- every step runs as the
+    // non-spinning k_reduce + k_apply pair and the xGMI set-up is refused
+    int scratch = 0;
+    HIPCHK(h, mdp_spin_kernels_scratch(&scratch));
+    if (scratch > 0) h->ra_cap = h->ra_batch_cap = 0;
   }
   if (hip_stream) {
     h->stream = (hipStream_t)hip_stream;
@@ -1350,7 +1395,7 @@ int mdp_make_index(mdp_handle* h, int32_t count, int32_t* idx_dev) {
 
 int mdp_sample_rows(mdp_handle* h, const int32_t* idx_dev, int32_t count, float* out_dev) {
   if (count <= 0) return 0;
-  ProfScope p(h, MDP_K_GATHER);
+  ProfScope p(h, MDP_K_GATHER, false);
   HIPCHK(h, mdp_launch_gather(h->replay, h->L.topo.row_stride, idx_dev, count, out_dev, h->stream));
   return 0;
 }
@@ -1706,6 +1751,12 @@ int mdp_dp_exchange_stats(mdp_handle* h, double out4[4], int32_t reset) {
     HIPCHK(h, hipMemsetAsync(&h->ctl->xw_ticks, 0, sizeof(w), h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
+  return 0;
+}
+
+int mdp_dp_exchange_stats_enable(mdp_handle* h, int32_t on) {
+  if (!h) return -1;
+  h->xw_stats = on != 0;
   return 0;
 }
 

@@ -291,7 +291,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       // once, log2 G dependent adds (a chain over the groups waited on each read)
       f32x4 g = red_tree<0, G>(red, col);
       MDP_STAMP(34);
-      if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ctr_use(ep_raw) + 1u, &a.ctl->xw_ticks);
+      if (f.phase == 3) g = xchg_chunk(f.xd, &a.ctl->fault, g, i0, act, ctr_use(ep_raw) + 1u, f.wstat);
       double ss = 0.0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -571,10 +571,30 @@ static bool mdp_ra_narrow(const FusedApplyArgs& f) { return MDP_RA_NARROW && f.a
 hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
   const dim3 grid(mdp_ra_grid(f) + (f.pf_count > 0 ? 1 : 0));
   if (mdp_ra_narrow(f))
-    hipLaunchKernelGGL(k_reduce_apply<256>, grid, dim3(256), 0, s, f);
+    mdp_launch(k_reduce_apply<256>, grid, dim3(256), 0, s, f);
   else
-    hipLaunchKernelGGL(k_reduce_apply<1024>, grid, dim3(1024), 0, s, f);
+    mdp_launch(k_reduce_apply<1024>, grid, dim3(1024), 0, s, f);
   return hipGetLastError();
+}
+
+// the largest private segment (scratch bytes per lane) of the kernels whose
+// workgroups spin on other workgroups of the same grid (the norm handshake, the
+// xGMI exchange and its probe).  Their correctness rests on the whole grid being
+// resident at once; waves that need scratch are dispatched only while the
+// queue's scratch slots last, so a spinning grid must not use any (the build
+// guard tools/check_scratch.py rejects it too; this is the run-time check)
+hipError_t mdp_spin_kernels_scratch(int* bytes) {
+  const void* ks[] = {(const void*)k_reduce_apply<256>, (const void*)k_reduce_apply<1024>,
+                      (const void*)k_reduce_apply_batch<256>, (const void*)k_reduce_apply_batch<1024>,
+                      (const void*)k_xchg_probe};
+  *bytes = 0;
+  for (const void* k : ks) {
+    hipFuncAttributes at;
+    const hipError_t e = hipFuncGetAttributes(&at, k);
+    if (e != hipSuccess) return e;
+    if ((int)at.localSizeBytes > *bytes) *bytes = (int)at.localSizeBytes;
+  }
+  return hipSuccess;
 }
 
 // co-resident k_reduce_apply workgroups per CU
@@ -589,9 +609,9 @@ hipError_t mdp_ra_batch_occupancy(int* per_cu) {
 
 hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s) {
   if (MDP_RA_NARROW && b.narrow)  // (no draw piece in a batch)
-    hipLaunchKernelGGL(k_reduce_apply_batch<256>, dim3(b.wg_start[b.count]), dim3(256), 0, s, b);
+    mdp_launch(k_reduce_apply_batch<256>, dim3(b.wg_start[b.count]), dim3(256), 0, s, b);
   else
-    hipLaunchKernelGGL(k_reduce_apply_batch<1024>, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
+    mdp_launch(k_reduce_apply_batch<1024>, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
   return hipGetLastError();
 }
 

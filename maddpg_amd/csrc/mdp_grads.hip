@@ -981,7 +981,7 @@ hipError_t launch_critic(const CriticArgs& a, int lds, hipStream_t s) {
     (void)hipGetLastError();
     attr = true;
   }
-  hipLaunchKernelGGL(k_critic_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(MDP_GEN_THREADS), lds, s, a);
+  mdp_launch(k_critic_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(MDP_GEN_THREADS), lds, s, a);
   return hipGetLastError();
 }
 template <int H>
@@ -993,7 +993,7 @@ hipError_t launch_actor(const ActorArgs& a, int lds, hipStream_t s) {
     (void)hipGetLastError();
     attr = true;
   }
-  hipLaunchKernelGGL(k_actor_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(MDP_GEN_THREADS), lds, s, a);
+  mdp_launch(k_actor_grad<H>, dim3((a.B + MDP_R - 1) / MDP_R), dim3(MDP_GEN_THREADS), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace

@@ -1140,7 +1140,7 @@ hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr, int 
     attr = true;
   }
   const int per = (a.B + MDP_R - 1) / MDP_R;
-  hipLaunchKernelGGL(kern, dim3(per * (a.multi > 1 ? a.multi : 1) + extra), dim3(512), lds, s, a);
+  mdp_launch(kern, dim3(per * (a.multi > 1 ? a.multi : 1) + extra), dim3(512), lds, s, a);
   return hipGetLastError();
 }
 }  // namespace

@@ -1,6 +1,7 @@
 // mdp_kernels.h -- kernel argument blocks and host-side launchers.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "mdp_topo.h"
@@ -169,6 +170,7 @@ struct FusedApplyArgs {
   const XchgDesc* xd;   // phase 3: device copy of the exchange descriptor
   int net_id;           // phase 3: 2 * agent + net (epoch counter)
   uint32_t* xstep;      // phase 3: Ctl::xstep[net_id], exchanges done for this net
+  uint64_t* wstat;      // phase 3: Ctl::xw_ticks when the exchange waits are stamped, else null
   // pf_count > 0: one extra (last) workgroup draws pf_count indices of the NEXT
   // round into pf_out, continuing the MT19937 stream (a piece of the draw the
   // fast kernels make beside the critic step; general-kernel configurations)
@@ -302,6 +304,27 @@ inline int lds_eval_bytes(int in, int H) {
   return 4 * (mdp_r4(R * ldx) + 2 * mdp_r4(R * ldh) + mdp_r4(R * 8));
 }
 
+// ---- per-launch timing (bench.py's kernel pass): when the host armed a
+// start/stop event pair for the next launch, that launch carries them on its
+// own dispatch packet (hipExtLaunchKernel), so their elapsed time is the
+// packet's begin -> end -- the interval rocprofv3 --kernel-trace reports --
+// with no marker packets of their own in between
+struct MdpLaunchEv {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+MdpLaunchEv& mdp_launch_ev();  // this host thread's armed pair (mdp_api.cpp)
+template <typename F, typename... Args>
+inline void mdp_launch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t s, Args... args) {
+  MdpLaunchEv& e = mdp_launch_ev();
+  if (e.start) {
+    const hipEvent_t a = e.start, z = e.stop;
+    e.start = e.stop = nullptr;
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, s, a, z, 0u, args...);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+  }
+}
+
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s);
@@ -322,6 +345,7 @@ struct RaBatch {
 };
 int mdp_ra_grid(const FusedApplyArgs& f);
 hipError_t mdp_ra_occupancy(int* per_cu);   // co-resident k_reduce_apply workgroups per CU
+hipError_t mdp_spin_kernels_scratch(int* bytes);  // largest scratch per lane of the spinning kernels
 // grid of the fused optimizer launch of (agent, net): the 256-parameter chunks
 // of the net, for the actor step the Polyak workgroups of the critic, one stats
 // workgroup (mirrors fused_args_for / apply_args / mdp_ra_grid)

@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(MDP_NT) void k_mlp_eval(EvalArgs a) {
 template <int H>
 static hipError_t launch_rollout_t(const RolloutArgs& a, int lds_bytes, hipStream_t s) {
   const int grid = (a.E + MDP_R - 1) / MDP_R + (a.pf_count > 0 ? 1 : 0);
-  hipLaunchKernelGGL(k_rollout<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
+  mdp_launch(k_rollout<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
@@ -1112,18 +1112,18 @@ hipError_t mdp_launch_eval(const EvalArgs& a, int H, int lds_bytes, hipStream_t 
 }
 hipError_t mdp_launch_apply(const ApplyArgs& a, hipStream_t s) {
   const int grid = a.blk[6] + (a.polyak ? a.oblk[6] : 0) + (a.stats_mode ? 1 : 0);
-  hipLaunchKernelGGL(k_apply, dim3(grid), dim3(256), 0, s, a);
+  mdp_launch(k_apply, dim3(grid), dim3(256), 0, s, a);
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
 hipError_t mdp_launch_reduce(const ReduceArgs& a, hipStream_t s) {
   const int grid = (int)((a.size * 8 + 255) / 256);
-  hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, s, a);
+  mdp_launch(k_reduce, dim3(grid), dim3(256), 0, s, a);
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
 hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_make_index, dim3(1), dim3(1024), 0, s, ctl, count, out);
+  mdp_launch(k_make_index, dim3(1), dim3(1024), 0, s, ctl, count, out);
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }

@@ -233,6 +233,7 @@ class Engine:
         file; no .meta -- the graph is built by code on both sides)."""
         if fmt == "tf1":
             from .common import tf_checkpoint as tfc
+            self._drop_stale(fname, keep="tf1")
             tfc.write_bundle(fname, tfc.tf1_from_state(self.state_dict()))
             d = os.path.dirname(os.path.abspath(fname + "x"))
             with open(os.path.join(d, "checkpoint"), "w") as fh:
@@ -245,18 +246,31 @@ class Engine:
         d = os.path.dirname(path)
         if d:
             os.makedirs(d, exist_ok=True)
+        self._drop_stale(fname, keep="npz")
         np.savez(path, **self.state_dict())
         return path
 
+    def _drop_stale(self, fname, keep):
+        """a save in one format removes the other format's files at the same
+        prefix, so a later --restore cannot pick up an older checkpoint"""
+        if keep == "npz":
+            for f in (fname + ".index", fname + ".data-00000-of-00001"):
+                if os.path.isfile(f):
+                    os.remove(f)
+        elif os.path.isfile(self.checkpoint_path(fname)):
+            os.remove(self.checkpoint_path(fname))
+
     def load_state(self, fname):
         """Restore from a TF1 tensor bundle at prefix `fname` (the reference's
-        tf.train.Saver checkpoint, tf_util.py:259-264) when `fname`.index
-        exists, else from the .npz save_state writes."""
+        tf.train.Saver checkpoint, tf_util.py:259-264) or from the .npz
+        save_state writes; when both exist (written by other tools), the newer
+        one."""
         from .common import tf_checkpoint as tfc
-        if tfc.is_bundle(fname):
+        path = self.checkpoint_path(fname)
+        if tfc.is_bundle(fname) and not (os.path.isfile(path) and
+                                         os.path.getmtime(path) > os.path.getmtime(fname + ".index")):
             self.load_state_dict(tfc.state_from_tf1(tfc.read_bundle(fname), self.n, self.SETS))
             return fname
-        path = self.checkpoint_path(fname)
         with np.load(path, allow_pickle=False) as z:
             self.load_state_dict({k: z[k] for k in z.files})
         return path
@@ -470,6 +484,11 @@ class Engine:
         out = (ctypes.c_double * 4)()
         self._c("mdp_dp_exchange_stats", out, 1 if reset else 0)
         return {"chunk_exchanges": int(out[0]), "mean_us": out[1], "max_us": out[2], "total_us": out[3]}
+
+    def dp_exchange_stats_enable(self, on=True):
+        """stamp the xGMI exchange waits in the optimizer launches issued while
+        enabled (mdp_dp_exchange_stats_enable; default off)"""
+        self._c("mdp_dp_exchange_stats_enable", 1 if on else 0)
 
     def param_checksum(self):
         """exact fingerprint of every replicated state region (weights, targets,

@@ -131,6 +131,17 @@ def test_trainer_facade_in_reference_loop(tmp_path):
         assert sd0.keys() == sd1.keys()
         for k in sd0:
             np.testing.assert_array_equal(sd1[k], sd0[k], err_msg=k)
+        # an npz save at the same prefix replaces the TF1 bundle: a later restore
+        # must not pick up the stale bundle (and the reverse)
+        eng.set_params(0, "actor", {k: v + 1 for k, v in eng.get_params(0, "actor").items()})
+        sd2 = eng.state_dict()
+        U.save_state(prefix)
+        assert not os.path.exists(prefix + ".index")
+        eng.set_params(0, "actor", {k: v * 0 for k, v in eng.get_params(0, "actor").items()})
+        U.load_state(prefix)
+        np.testing.assert_array_equal(eng.state_dict()["agent_0/actor/W1"], sd2["agent_0/actor/W1"])
+        U.save_state(prefix, fmt="tf1")
+        assert not os.path.exists(eng.checkpoint_path(prefix))
 
 
 @pytest.mark.parametrize("scenario,extra", [

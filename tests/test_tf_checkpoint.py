@@ -127,3 +127,13 @@ def test_beta_powers_found_under_either_suffix():
     del t["agent_0/q_func/fully_connected/weights"]
     with pytest.raises(KeyError, match="q_func/fully_connected/weights"):
         tfc.state_from_tf1(t, 1, ("actor", "critic"))
+
+
+def test_shape_unknown_rank_field():
+    """TensorShapeProto field 3 (unknown_rank) present but false is a known-rank
+    shape; only unknown_rank = true is refused"""
+    dims = tfc._pf_bytes(2, tfc._pf_varint(1, 3)) + tfc._pf_bytes(2, tfc._pf_varint(1, 4))
+    e = tfc._parse_entry(tfc._pf_varint(1, 1) + tfc._pf_bytes(2, dims + tfc._pf_varint(3, 0)))
+    assert e["shape"] == [3, 4]
+    with pytest.raises(ValueError, match="unknown-rank"):
+        tfc._parse_entry(tfc._pf_varint(1, 1) + tfc._pf_bytes(2, tfc._pf_varint(3, 1)))

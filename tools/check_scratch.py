@@ -5,7 +5,12 @@ except the general critic kernels, whose register spills are known.
 A private array the compiler could not keep in registers (e.g. a loop over it
 that stayed rolled) lands in scratch: slow, and a 1024-thread optimizer launch
 with 336 B of scratch per lane faulted the GPU inside the captured train-step
-graph.  Run by the Makefile after the link:
+graph.  The allowed kernels never wait on another workgroup; the optimizer
+launches do (norm handshake, xGMI exchange), and waves that need scratch are
+dispatched only while the queue's scratch slots last, so a spinning grid with
+scratch may not be co-resident.  mdp_create re-checks the spinning kernels at
+run time (mdp_spin_kernels_scratch) and disables the spinning launches if any
+has a private segment.  Run by the Makefile after the link:
 
     python3 tools/check_scratch.py maddpg_amd/libmaddpg_hip.so
 """

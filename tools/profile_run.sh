@@ -17,4 +17,9 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format 
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/mfma -o run --output-format csv -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage --no-configs2 > $O/mfma.json 2> $O/mfma.err
+# 6) wave-state counters of every kernel (quad-cycles): parked at s_waitcnt / barrier, issue-stalled,
+#    LDS-issue-stalled, active; VALU / LDS activity and bank conflicts (tools/profile_summary.py --sq)
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY \
+    SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT -d $O/sq -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-throughput-figure --no-gather-stage --no-configs2 > $O/sq.json 2> $O/sq.err
 echo "profile $TAG done"

@@ -21,6 +21,9 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format 
     python3 bench.py $Q $S5 --steps 2 --warmup 1 > $O/write.json 2> $O/write.err
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/mfma -o run --output-format csv -- \
     python3 bench.py $Q $S5 --steps 2 --warmup 1 > $O/mfma.json 2> $O/mfma.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY \
+    SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT -d $O/sq -o run --output-format csv -- \
+    python3 bench.py $Q $S5 --steps 2 --warmup 1 > $O/sq.json 2> $O/sq.err
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-gather-stage --no-configs2 $S5 --steps 20 --warmup 3 \
     > $O/bench.json 2> $O/bench.err
 echo "profile ${TAG}_s5 done"

@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--bench")
     ap.add_argument("--mfma", help="rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE pass")
+    ap.add_argument("--sq", help="rocprofv3 --pmc pass of the SQ wave-state counters (profile_run.sh pass 6)")
     ap.add_argument("--clock-ghz", type=float, default=2.3, help="shader clock for the MFMA busy fraction")
     ap.add_argument("--config-key", default=None)
     a = ap.parse_args()
@@ -96,7 +97,26 @@ def main():
             for k, v in mf.items():
                 allj.setdefault(key, {}).setdefault(k, {}).update(v)
             json.dump(allj, open(path, "w"), indent=1, sort_keys=True)
-    print(json.dumps({"tag": a.tag, "config_key": key, "avg_ns": avg_ns, "pmc": out, "mfma": mf}, indent=1))
+    sq = {}
+    if a.sq:
+        names = ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY",
+                 "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT"]
+        got = {n: counters(a.sq, n) for n in names}
+        kern = sorted(set().union(*[set(g) for g in got.values()]))
+        with open(os.path.join(prof, f"{a.tag}_sq.csv"), "w") as fp:
+            # per launch; wave-state counters in quad-cycles summed over every wave of the launch;
+            # the shares are of SQ_WAVE_CYCLES (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES)
+            fp.write("kernel,avg_ns," + ",".join(names) +
+                     ",wait_any_share,wait_inst_any_share,wait_inst_lds_share,active_share\n")
+            for k in kern:
+                v = {n: got[n].get(k) for n in names}
+                wc = v["SQ_WAVE_CYCLES"] or 0.0
+                sh = [(v[n] or 0.0) / wc if wc else 0.0 for n in
+                      ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY")]
+                sq[k] = dict(v, shares=sh)
+                fp.write(f"{k},{avg_ns.get(k, '')}," + ",".join("" if v[n] is None else f"{v[n]:.0f}" for n in names)
+                         + "," + ",".join(f"{x:.4f}" for x in sh) + "\n")
+    print(json.dumps({"tag": a.tag, "config_key": key, "avg_ns": avg_ns, "pmc": out, "mfma": mf, "sq": sq}, indent=1))
 
 
 if __name__ == "__main__":
