@@ -195,7 +195,11 @@ def load_pmc(kernel, config_key):
     if not os.path.exists(path):
         return {}
     try:
-        return json.load(open(path)).get(config_key, {}).get(kernel) or {}
+        cfg = json.load(open(path)).get(config_key, {})
+        out = dict(cfg.get(kernel) or {})
+        if out and cfg.get("_source"):
+            out["_source"] = "profiles/" + cfg["_source"]
+        return out
     except Exception:
         return {}
 
@@ -497,6 +501,7 @@ def main():
             pmc["hbm_bytes_per_launch"] = sum(p["hbm_bytes_per_launch"] for p in parts)
         if all(p.get("avg_ns") for p in parts):
             pmc["avg_ns"] = sum(p["avg_ns"] for p in parts)
+            pmc["_source"] = parts[0].get("_source")
             if all(p.get("mfma_busy_frac") is not None for p in parts):
                 pmc["mfma_busy_frac"] = sum(p["mfma_busy_frac"] * p["avg_ns"] for p in parts) / pmc["avg_ns"]
     elif roof is not None:
@@ -508,11 +513,25 @@ def main():
             roof["mfma_busy_frac_rocprof"] = round(pmc["mfma_busy_frac"], 5)
         if pmc.get("avg_ns"):
             # the committed rocprofv3 --kernel-trace --stats average of the same kernel and
-            # workload (profiles/): the live packet-event figure above must agree with it
-            roof["rocprof_avg_launch_ms"] = round(pmc["avg_ns"] * 1e-6, 6)
-            roof["frac_at_rocprof_duration"] = round(
-                roof["frac"] * roof["avg_launch_ms"] / roof["rocprof_avg_launch_ms"], 6)
-            roof["live_vs_rocprof_duration"] = round(roof["avg_launch_ms"] / roof["rocprof_avg_launch_ms"], 4)
+            # workload (profiles/, mostly graph-replayed launches) is the headline duration; the
+            # live packet-event figure (eager launches of the kernel pass) is kept beside it and
+            # must agree: eager launches run ~3-5 % shorter than graph-replayed ones (the trace
+            # shows the same split), so a gap beyond 10 % means the profile is stale -> live
+            live_ms = roof["avg_launch_ms"]
+            prof_ms = pmc["avg_ns"] * 1e-6
+            roof["rocprof_avg_launch_ms"] = round(prof_ms, 6)
+            roof["live_avg_launch_ms"] = live_ms
+            roof["live_achieved"] = roof["achieved"]
+            roof["live_frac"] = roof["frac"]
+            roof["live_vs_rocprof_duration"] = round(live_ms / prof_ms, 4)
+            if abs(live_ms / prof_ms - 1.0) <= 0.10:
+                scale = live_ms / prof_ms
+                roof["avg_launch_ms"] = prof_ms
+                roof["achieved"] = round(roof["achieved"] * scale, 4)
+                roof["frac"] = round(roof["frac"] * scale, 6)
+                roof["duration_source"] = f"rocprofv3 --kernel-trace --stats average ({pmc.get('_source', 'profiles')})"
+            else:
+                roof["duration_source"] = "live packet events (the committed rocprof summary is stale: >10 % apart)"
         if roof.get("traffic") and roof.get("algorithmic_bytes_per_launch"):
             # counted HBM bytes (2*FETCH + WRITE) over the algorithmic bytes: the re-read /
             # write-back excess of the launch (partial-gradient slabs, hand-off blocks, weights per XCD)
