@@ -607,7 +607,11 @@ ApplyArgs apply_args(mdp_handle* h, int agent, int net, float scale, bool tp = f
   chunks(a.other, a.oblk);
   a.slab = nullptr;
   a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
+#ifdef MDP_EXP_R32  // timing-only build: 32-row gradient workgroups leave half the partials
+  a.nwg = (h->L.nwg + 1) / 2;
+#else
   a.nwg = h->L.nwg;
+#endif
   a.scale = scale;
   a.clip = h->cfg.grad_clip;
   a.lr = h->cfg.lr;

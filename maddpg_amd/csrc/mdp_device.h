@@ -20,6 +20,24 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// one fp32 MFMA step, D = A x B + C over a 16x16 tile with k = 4 (exact fp32:
+// the bitwise fmaf chain, MI355X_MICROARCH.md).  MDP_EXP_R32 (timing-only
+// build of the register-resident kernels, tools/build_variant.sh): every step
+// is issued a second time with an opaque zero A operand into the same
+// accumulator -- the MFMA work of a 32-row tile on the same weight fragment,
+// results unchanged (0 x b + c == c) -- to size 32-row workgroups at S2
+#ifdef MDP_EXP_R32
+__device__ __forceinline__ f32x4 mdp_mfma_x2(float a, float b, f32x4 c) {
+  float z = 0.f;
+  asm volatile("" : "+v"(z));
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(z, b, c, 0, 0, 0);
+}
+#define MDP_MFMA(a, b, c) mdp_mfma_x2((a), (b), (c))
+#else
+#define MDP_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+#endif
+
 // diagnostic build only (-DMDP_STAMPS): wall-clock stamps of workgroup 0
 #ifdef MDP_STAMPS
 __device__ unsigned long long g_mdp_stamps[64];
@@ -282,7 +300,7 @@ __device__ __forceinline__ f32x4 mfma_chunk(f32x4 acc, const float (&w)[MDP_KC],
 #pragma unroll
   for (int s = 0; s < MDP_KC; ++s) {
     if (c0 + 4 * s < K)  // wave-uniform
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+      acc = MDP_MFMA(x[s], w[s], acc);
   }
   return acc;
 }
@@ -373,7 +391,7 @@ __device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const 
       }
 #pragma unroll
       for (int s = 0; s < MDP_KC; ++s)
-        if (c0 + 4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+        if (c0 + 4 * s < K) acc = MDP_MFMA(x[s], w[s], acc);
     }
     const float bias = b[c];
     if (r < nout) {
@@ -394,7 +412,7 @@ __device__ __forceinline__ void head_mfma(const float* X, int ldx, int K, const 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < KS; ++s)
-    if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+    if (4 * s < K) acc = MDP_MFMA(x[s], w[s], acc);
   if (r < nout) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[(kq * 4 + i) * ldo + r] = acc[i] + bias;
@@ -422,7 +440,7 @@ __device__ __forceinline__ void head_acc(const float (&w)[KS], float bias, const
   for (int s = 0; s < KS; ++s) x[s] = X[r * ldx + 4 * s + kq];
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+  for (int s = 0; s < KS; ++s) acc = MDP_MFMA(x[s], w[s], acc);
   if (r < nout) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[(kq * 4 + i) * ldo + r] = acc[i] + bias;
@@ -531,8 +549,8 @@ __device__ __forceinline__ void mfma_chunk2(f32x4& acc_a, const float (&xa)[MDP_
                                             f32x4& acc_b, const float (&xb)[MDP_KC], const float (&wb)[MDP_KC], int nb) {
 #pragma unroll
   for (int s = 0; s < MDP_KC; ++s) {
-    if (s < na) acc_a = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], wa[s], acc_a, 0, 0, 0);
-    if (s < nb) acc_b = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s], wb[s], acc_b, 0, 0, 0);
+    if (s < na) acc_a = MDP_MFMA(xa[s], wa[s], acc_a);
+    if (s < nb) acc_b = MDP_MFMA(xb[s], wb[s], acc_b);
   }
 }
 
@@ -652,7 +670,7 @@ __device__ __forceinline__ void wave_layer(const float* X, int ldx, int K, const
     for (int s = 0; s < MDP_KC; ++s) {
       if (s < ns) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[t][s], acc[t], 0, 0, 0);
+        for (int t = 0; t < NT; ++t) acc[t] = MDP_MFMA(x[s], w[t][s], acc[t]);
       }
     }
   }
@@ -703,7 +721,7 @@ __device__ __forceinline__ void wave_dgrad(const float* dY, int ldy, int N, cons
     for (int s = 0; s < MDP_KC; ++s) {
       if (c0 + 4 * s < N) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[t][s], acc[t], 0, 0, 0);
+        for (int t = 0; t < NT; ++t) acc[t] = MDP_MFMA(x[s], w[t][s], acc[t]);
       }
     }
   }
@@ -733,7 +751,7 @@ __device__ __forceinline__ void dgrad_tiles(const float* dY, int ldy, int N, con
       load_afrag(x, dY, ldy, r, c0, N, kq);
 #pragma unroll
       for (int s = 0; s < MDP_KC; ++s)
-        if (c0 + 4 * s < N) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+        if (c0 + 4 * s < N) acc = MDP_MFMA(x[s], w[s], acc);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -882,7 +900,7 @@ __device__ __forceinline__ void rf_acc(f32x4 (&acc)[4], const float* X, int ldx,
   for (int s = 0; s < KS; ++s) {
     if (4 * s < K) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s][t], acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) acc[t] = MDP_MFMA(x[s], w[s][t], acc[t]);
     }
   }
 }
@@ -923,7 +941,7 @@ __device__ __forceinline__ f32x4 rh_acc(const float* X, int ldx, const float (&w
   __builtin_amdgcn_sched_barrier(0);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+  for (int s = 0; s < 16; ++s) acc = MDP_MFMA(x[s], w[s], acc);
   return acc;
 }
 
@@ -976,7 +994,7 @@ __device__ __forceinline__ void rt_acc(f32x4& acc, const float* X, int ldx, int 
   __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMA chain
 #pragma unroll
   for (int s = 0; s < KS; ++s)
-    if (4 * s < K) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s], acc, 0, 0, 0);
+    if (4 * s < K) acc = MDP_MFMA(x[s], w[s], acc);
 }
 
 // transposed tile for dX = dY @ W^T (W[K][64] row-major): output column kk = W row,
@@ -999,7 +1017,7 @@ __device__ __forceinline__ f32x4 rdg_acc(const float* dY, int ldy, const f32x4 (
   __builtin_amdgcn_sched_barrier(0);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s >> 2][s & 3], acc, 0, 0, 0);
+  for (int s = 0; s < 16; ++s) acc = MDP_MFMA(x[s], w[s >> 2][s & 3], acc);
   return acc;
 }
 
@@ -1118,7 +1136,7 @@ __device__ __forceinline__ void wgrad_multi(const WgJob& j0, const WgJob& j1, co
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < T; ++s) acc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(g[s][i], a[s][i], acc[s], 0, 0, 0);
+      for (int s = 0; s < T; ++s) acc[s] = MDP_MFMA(g[s][i], a[s][i], acc[s]);
 #pragma unroll
     for (int s = 0; s < T; ++s)
       if (krem[s]) slab_st4(dst[s], acc[s]);
@@ -1141,7 +1159,7 @@ __device__ __forceinline__ void wgrad_waves(const float* X, int ldx, int K, cons
       const float xv = X[row * ldx + fc];
       const float a = feat < K ? xv : 0.f;
       const float g = dY[row * ldy + nt * 16 + r];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(g, a, acc, 0, 0, 0);  // transposed tile
+      acc = MDP_MFMA(g, a, acc);  // transposed tile
     }
     if (feat < K) slab_st4(dW + feat * N + nt * 16 + kq * 4, acc);
   }

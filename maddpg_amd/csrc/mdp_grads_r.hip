@@ -38,6 +38,14 @@
 #include "mdp_kernels.h"
 #include "mdp_mt.h"
 
+// row tiles per workgroup for the grid: 16 rows (MDP_R); the timing-only
+// MDP_EXP_R32 build sizes 32-row workgroups (half the grid, see MDP_MFMA)
+#ifdef MDP_EXP_R32
+#define MDP_RW 32
+#else
+#define MDP_RW MDP_R
+#endif
+
 // diagnostic build: every workgroup's start (wave 0) and per-wave end of the
 // last critic (k = 0) / actor (k = 1) launch -- which role ends the launch
 #ifdef MDP_STAMPS
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   __shared__ int dq_ready;      // wave 4 wrote dL/dq (the dh1 tiles of waves 0..3 wait for it)
   int agent = a.agent, bx = blockIdx.x;
   if (a.apre) {  // workgroups [B/16, 2 B/16): the actor step's forward (strict mode only)
-    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    const int nwg = (a.B + MDP_RW - 1) / MDP_RW;
     if (bx >= nwg) {
       MDP_TL_ROLE(0, 1);
       actor_pre_tile(a, lds, &rows_ready, bx - nwg);
@@ -451,7 +459,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     }
   }
   if (a.multi > 1) {  // throughput mode: every agent's critic step in this launch
-    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    const int nwg = (a.B + MDP_RW - 1) / MDP_RW;
     agent = bx / nwg;
     bx -= agent * nwg;
   }
@@ -749,7 +757,7 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     __syncthreads();  // B4
     f32x4 u = {0.f, 0.f, 0.f, 0.f};  // u tile `wave` (columns 16 wave .. 16 wave + 15), rdg_acc's chain
 #pragma unroll
-    for (int q = 0; q < 16; ++q) u = __builtin_amdgcn_mfma_f32_16x16x4f32(vx[q], wt[q >> 2][q & 3], u, 0, 0, 0);
+    for (int q = 0; q < 16; ++q) u = MDP_MFMA(vx[q], wt[q >> 2][q & 3], u);
     lds_wait(&dq_ready, 1);
     {
       const int col = 16 * wave + r;
@@ -767,6 +775,9 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     // and needed late); waves 0..3 start on their weight loads at once
     if (post) load_rows16_part(a.cpre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 256, 256);
     else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 256, 256);
+#ifdef MDP_EXP_R32  // the second 16-row tile's rows (timing only: same buffer)
+    gather_rows16_part(a.replay, T.row_stride, idx, min(r0 + MDP_R, a.B - MDP_R), MDP_R, rowbuf, ldr, 256, 256);
+#endif
     lds_signal(&rows_ready);
 #ifdef MDP_STAMPS
     if (tt == 0) {
@@ -892,7 +903,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   MDP_TL(a.ctl, 2, 0);
   int agent = a.agent, bx = blockIdx.x;
   if (a.cpre) {  // workgroups [B/16, 2 B/16): the next critic step's independent work (strict mode)
-    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    const int nwg = (a.B + MDP_RW - 1) / MDP_RW;
     if (bx >= nwg) {
       MDP_TL_ROLE(2, 1);
       critic_pre_tile(a, lds, &rows_ready, bx - nwg);
@@ -901,7 +912,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     }
   }
   if (a.multi > 1) {  // throughput mode: every agent's actor step in this launch
-    const int nwg = (a.B + MDP_R - 1) / MDP_R;
+    const int nwg = (a.B + MDP_RW - 1) / MDP_RW;
     agent = bx / nwg;
     bx -= agent * nwg;
   }
@@ -1034,6 +1045,9 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       if (wave > 1) {
         if (a.apre) load_rows16_part(a.apre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 128, 384);
         else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
+#ifdef MDP_EXP_R32
+        gather_rows16_part(a.replay, T.row_stride, idx, min(r0 + MDP_R, a.B - MDP_R), MDP_R, rowbuf, ldr, 128, 384);
+#endif
       }
       if (wave > 1) lds_signal(&rows_ready);
       const int k0 = KC * (wave - 1);  // this wave's third of the replay-part contraction
@@ -1096,6 +1110,9 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     // waves 2..7 gather the replay rows (first); waves 0, 1 start on their weights at once
     if (a.apre) load_rows16_part(a.apre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 128, 384);
     else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
+#ifdef MDP_EXP_R32
+    gather_rows16_part(a.replay, T.row_stride, idx, min(r0 + MDP_R, a.B - MDP_R), MDP_R, rowbuf, ldr, 128, 384);
+#endif
     lds_signal(&rows_ready);
     f32x4 wc[4], wa[4];
     lds_wait(&fwd_issued, 4);  // the critic forward's loads go first
@@ -1139,7 +1156,7 @@ hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr, int 
     (void)hipGetLastError();
     attr = true;
   }
-  const int per = (a.B + MDP_R - 1) / MDP_R;
+  const int per = (a.B + MDP_RW - 1) / MDP_RW;
   mdp_launch(kern, dim3(per * (a.multi > 1 ? a.multi : 1) + extra), dim3(512), lds, s, a);
   return hipGetLastError();
 }
@@ -1147,14 +1164,14 @@ hipError_t launch_r(K kern, const A& a, int lds, hipStream_t s, bool& attr, int 
 
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s) {
   static bool attr = false;
-  const int per = (a.B + MDP_R - 1) / MDP_R;
+  const int per = (a.B + MDP_RW - 1) / MDP_RW;
   // grid: critic row tiles | actor-forward row tiles (a.apre) | the index draw (pf_count; last)
   return launch_r(k_critic_grad_r, a, lds_bytes, s, attr, (a.apre ? per : 0) + (a.pf_count > 0 ? 1 : 0));
 }
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s) {
   static bool attr = false;
   // grid: actor row tiles | the next critic step's row tiles (a.cpre)
-  return launch_r(k_actor_grad_r, a, lds_bytes, s, attr, a.cpre ? (a.B + MDP_R - 1) / MDP_R : 0);
+  return launch_r(k_actor_grad_r, a, lds_bytes, s, attr, a.cpre ? (a.B + MDP_RW - 1) / MDP_RW : 0);
 }
 
 #ifdef MDP_TIMELINE

@@ -9,7 +9,7 @@ D=/tmp/mdp_variant_$NAME
 rm -rf $D; mkdir -p $D
 mkdir -p $D/maddpg_amd $D/include $D/tools; cp -r maddpg_amd/csrc $D/maddpg_amd/csrc; cp include/*.h $D/include/; cp tools/check_scratch.py $D/tools/
 rm -rf $D/maddpg_amd/csrc/build
-make -s -C $D/maddpg_amd/csrc -j8 CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wall -Wno-unused-function $*" OUT=$D/lib.so HDR= > /dev/null
+make -s -C $D/maddpg_amd/csrc -j8 CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wall -Wno-unused-function $*" OUT=$D/lib.so HDR= $D/lib.so > /dev/null
 cp $D/lib.so maddpg_amd/libmaddpg_hip_$NAME.so
 rm -rf $D
 echo "built variant $NAME ($*) -> maddpg_amd/libmaddpg_hip_$NAME.so"
