@@ -35,7 +35,7 @@ extern "C" {
 #define MDP_MAX_AGENTS 8
 #define MDP_ACT_DIM 5          /* MPE Discrete(dim_p*2+1) action spaces */
 #define MDP_MAX_UNITS 256      /* largest --num-units (train.py:24) */
-#define MDP_ABI_VERSION 3
+#define MDP_ABI_VERSION 4
 
 enum mdp_scenario {
     MDP_SCN_NONE = 0,          /* trainer only (no device env) */

@@ -22,7 +22,7 @@ MAX_AGENTS = 8
 ACT_DIM = 5
 BENCH_W = 8   # MDP_BENCH_W: floats per agent benchmark_data record
 MAX_UNITS = 256  # MDP_MAX_UNITS: largest --num-units
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 SCN = {"none": 0, "simple": 1, "simple_spread": 2, "simple_adversary": 3, "simple_tag": 4}
 WHICH = {"actor": 0, "critic": 1, "tgt_actor": 2, "tgt_critic": 3, "m_actor": 4, "v_actor": 5,
