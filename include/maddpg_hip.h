@@ -160,6 +160,15 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev,
                const float* u_tgt_dev, const float* u_act_dev);
 /* gates of maddpg.py:162-165; returns 1 (skip) or 0 (train) */
 int mdp_update_gate(mdp_handle* h, int64_t t);
+/* MADDPGAgentTrainer.update(agents, t) as one call (maddpg.py:161-196), the
+ * signature SURVEY.md 8b sketches: the gates at train step t (1 = skipped,
+ * the reference's `return None`, nothing drawn), else the update on idx_dev
+ * (B indices, or NULL: drawn from the device MT stream, replay_buffer.py:46-47)
+ * with u_dev (NULL, or [n_agents][B][5] target-actor uniforms followed by
+ * [B][5] actor-loss uniforms) and the 6 stats [q_loss, p_loss, mean y,
+ * mean r, mean Q', std y] in stats_out (synchronous); 0 = trained, <0 error */
+int mdp_agent_update(mdp_handle* h, int32_t agent, int64_t t, const int32_t* idx_dev, const float* u_dev,
+                     double stats_out[6]);
 /* update round: all agents in order (train.py:158-161), indices from the MT stream.
  * Replayed from a captured hipGraph after the first round (see mdp_set_graphs). */
 int mdp_update_round(mdp_handle* h);

@@ -1486,6 +1486,18 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
   return do_update(h, agent, idx, u_tgt_dev, u_act_dev);
 }
 
+int mdp_agent_update(mdp_handle* h, int32_t agent, int64_t t, const int32_t* idx_dev, const float* u_dev,
+                     double stats_out[6]) {
+  if (!h || !stats_out) return -1;
+  if (bad_agent(h, agent)) return -1;
+  if (mdp_update_gate(h, t)) return 1;
+  const float* u_tgt = u_dev;
+  const float* u_act = u_dev ? u_dev + (int64_t)h->cfg.n_agents * h->cfg.batch_size * MDP_ACT_DIM : nullptr;
+  const int rc = mdp_update(h, agent, idx_dev, u_tgt, u_act);
+  if (rc) return rc;
+  return mdp_get_stats(h, agent, stats_out);
+}
+
 // One strict round.  Agent i's critic step is split around agent i-1's update
 // when critic_pre_ok: its independent part rides in i-1's actor launch.
 // carry_in: the previous round's last actor launch already did agent 0's part

@@ -384,6 +384,20 @@ class Engine:
         self._keep = args
         self.sync_out()
 
+    def agent_update(self, agent, t, idx=None, u=None):
+        """MADDPGAgentTrainer.update(agents, t) in one C call (mdp_agent_update):
+        None below the gates (maddpg.py:162-165), else the 6 stats.  u: None or
+        [n * B * 5 target-actor uniforms | B * 5 actor-loss uniforms] (flat)."""
+        args = []
+        for a, dt in ((idx, torch.int32), (u, torch.float32)):
+            args.append(None if a is None else a.to(self.device, dt).contiguous().reshape(-1))
+        out = (ctypes.c_double * 6)()
+        self.sync_in()
+        rc = self._c("mdp_agent_update", int(agent), int(t), *[self._ptr(a) for a in args], out)
+        self._keep = args
+        self.sync_out()
+        return None if rc == 1 else list(out)
+
     def update_gate(self, t):
         return self._c("mdp_update_gate", int(t))
 

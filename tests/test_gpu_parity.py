@@ -780,3 +780,37 @@ def test_split_steps_bit_identical(monkeypatch, dims, local_q):
                 np.testing.assert_array_equal(a[k], b[k], err_msg=f"{i} {w} {k} split vs unsplit")
                 np.testing.assert_array_equal(a[k], d[k], err_msg=f"{i} {w} {k} round vs per-agent")
         np.testing.assert_array_equal(on.stats(i), off.stats(i))
+
+
+def test_agent_update_literal_abi_vs_oracle():
+    """mdp_agent_update (SURVEY 8b's one-call update: gates at t, update, 6 stats)
+    against mdp_update + mdp_get_stats and the oracle: below the replay gate
+    and off the t % 100 cadence it returns None without drawing (the device MT
+    state is unchanged); on the cadence it trains with the injected indices and
+    uniforms and returns the oracle's stats."""
+    dims, B = [18, 18, 18], 256
+    L = B * 25 + 100                      # past the gate: len >= B * max_episode_len
+    c = synthetic_trainer_case(dims, B, L, seed=71)
+    rows = joint_rows(c["data"], dims)
+    engines = []
+    for n_rows in (B * 25 - 1, L):
+        e = Engine(dims, batch_size=B, capacity=L + 7)
+        e.add_rows(torch.from_numpy(rows[:n_rows]))
+        for i, p in enumerate(c["params"]):
+            for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+                e.set_params(i, w, p[w])
+        engines.append(e)
+    eng, eng2 = engines
+    st0, st1 = eng.get_rng_state(), eng2.get_rng_state()
+    assert eng.agent_update(0, 100) is None                     # len < B * 25: maddpg.py:162-163
+    assert eng2.agent_update(0, 101) is None                    # t % 100 != 0: maddpg.py:164-165
+    assert np.array_equal(eng.get_rng_state(), st0) and np.array_equal(eng2.get_rng_state(), st1)
+    agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
+    for i in range(3):
+        u = np.concatenate([c["u_tgt"][i].ravel(), c["u_act"][i].ravel()])
+        got = eng2.agent_update(i, 200, idx=torch.from_numpy(c["idx"][i]), u=torch.from_numpy(u))
+        want, _ = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i])
+        assert got is not None and len(got) == 6
+        assert got == eng2.stats(i)
+        assert abs(got[0] - want[0]) <= 1e-5 * abs(want[0]) + 1e-7, (got, want)
+        np.testing.assert_allclose(got[1:], want[1:], rtol=2e-5, atol=2e-6)
