@@ -810,12 +810,22 @@ __device__ __forceinline__ void load_rows16_part(const float* __restrict__ block
   }
 }
 // rowbuf's 16 rows -> a contiguous [16][stride] block (all threads)
+// 16-B store of a split-step hand-off block (apre / cpre and their row
+// blocks, read by the next launch); MDP_WT_HANDOFF: write-through (sc1)
+__device__ __forceinline__ void handoff_st4(float* p, f32x4 v) {
+#ifdef MDP_WT_HANDOFF
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#else
+  *reinterpret_cast<f32x4*>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ void store_rows16(const float* rowbuf, int ldr, int stride, float* __restrict__ block) {
   const int v4 = stride >> 2;
   for (int e = threadIdx.x; e < MDP_R * v4; e += blockDim.x) {
     const int r = e / v4, c4 = e - r * v4;
     const float* sp = rowbuf + r * ldr + c4 * 4;
-    *reinterpret_cast<float4*>(block + (int64_t)r * stride + c4 * 4) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+    handoff_st4(block + (int64_t)r * stride + c4 * 4, f32x4{sp[0], sp[1], sp[2], sp[3]});
   }
 }
 
@@ -1053,7 +1063,9 @@ __device__ __forceinline__ double sum16(double v) {  // lanes 0..15 (every lane 
 #define MDP_NT_SLAB 0
 #endif
 __device__ __forceinline__ void slab_st(float* p, float v) {
-#if MDP_NT_SLAB == 2
+#if MDP_NT_SLAB == 3  // write-through vector store (global_store_dword sc1): no dirty L2 line at the kernel end
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#elif MDP_NT_SLAB == 2
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through (sc1)
 #elif MDP_NT_SLAB
   __builtin_nontemporal_store(v, p);
@@ -1062,7 +1074,9 @@ __device__ __forceinline__ void slab_st(float* p, float v) {
 #endif
 }
 __device__ __forceinline__ void slab_st4(float* p, f32x4 v) {
-#if MDP_NT_SLAB == 2
+#if MDP_NT_SLAB == 3  // one 16-B write-through store (the round-3 "sc1" variant was four 4-B ones)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#elif MDP_NT_SLAB == 2
 #pragma unroll
   for (int j = 0; j < 4; ++j) __hip_atomic_store(p + j, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #elif MDP_NT_SLAB

@@ -252,7 +252,7 @@ __device__ __forceinline__ void actor_pre_tile(const CriticArgs& a, float* lds, 
   __syncthreads();
   float* dst = a.apre + (int64_t)r0 * MDP_APRE_W;
   for (int q = threadIdx.x; q < MDP_R * MDP_APRE_W / 4; q += blockDim.x)
-    *reinterpret_cast<f32x4*>(dst + 4 * q) = *reinterpret_cast<const f32x4*>(apre_lds(q, h1a, h2a, lg, av));
+    handoff_st4(dst + 4 * q, *reinterpret_cast<const f32x4*>(apre_lds(q, h1a, h2a, lg, av)));
   store_rows16(rowbuf, ldr, T.row_stride, a.apre_rows + (int64_t)r0 * T.row_stride);
 }
 // one wave stores 16 rows x ncols (a multiple of 4) of an LDS tile into the
@@ -261,7 +261,7 @@ __device__ __forceinline__ void wave_store_cols16(const float* src, int ld, floa
   const int lane = threadIdx.x & 63, n4 = ncols >> 2;
   for (int e = lane; e < MDP_R * n4; e += 64) {
     const int r = e / n4, c = 4 * (e - r * n4);
-    *reinterpret_cast<f32x4*>(dst + r * MDP_CPRE_W + c0 + c) = *reinterpret_cast<const f32x4*>(src + r * ld + c);
+    handoff_st4(dst + r * MDP_CPRE_W + c0 + c, *reinterpret_cast<const f32x4*>(src + r * ld + c));
   }
 }
 // first MFMA k-step (of 4 inputs) of the target critic's a~ part that holds a
@@ -368,7 +368,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
       for (int e = threadIdx.x; e < MDP_R * v4; e += 3 * 64) {
         const int rr = e / v4, c4 = e - rr * v4;
         const float* sp = rowbuf + rr * ldr + c4 * 4;
-        *reinterpret_cast<float4*>(rb + (int64_t)rr * T.row_stride + c4 * 4) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+        handoff_st4(rb + (int64_t)rr * T.row_stride + c4 * 4, f32x4{sp[0], sp[1], sp[2], sp[3]});
       }
     }
   } else if (wave == 3) {
@@ -401,7 +401,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
     CPRE_T(3);
     wave_store_cols16(h1c, LH, dst, 0, RH);
     wave_store_cols16(h2c, LH, dst, RH, RH);
-    if ((lane & 3) == 0) *reinterpret_cast<f32x4*>(dst + (lane >> 2) * MDP_CPRE_W + 3 * RH) = f32x4{q, 0.f, 0.f, 0.f};
+    if ((lane & 3) == 0) handoff_st4(dst + (lane >> 2) * MDP_CPRE_W + 3 * RH, f32x4{q, 0.f, 0.f, 0.f});
   } else {
     const int tt = wave - 4, col = 16 * tt + r;
     gather_rows16_part(a.replay, T.row_stride, a.cpre_idx, r0, nvalid, rowbuf, ldr, 256, 256);
