@@ -284,3 +284,24 @@ def test_headless_display_frames(tmp_path):
     idat = raw[raw.index(b"IDAT") + 4: raw.index(b"IEND") - 8]
     assert len(zlib.decompress(idat)) == hgt * (1 + 3 * wdt)
     assert np.load(tmp_path / "d" / "positions.npz")["pos"].shape == (3, 6, 2)
+
+
+def test_bench_algorithmic_model_matches_survey():
+    """bench.py's roofline model against SURVEY 8d's per-unit figures: S2 critic
+    step 95.4 MFLOP / 0.863 MB, actor step 0.500 MB (58.6 MFLOP by the kernels'
+    MAC count), S5 critic step 2,009 MFLOP / 6.40 MB; and the roofline fields
+    the line carries (frac from the committed rocprof duration, live beside it)."""
+    import types
+    import bench
+
+    s2 = types.SimpleNamespace(num_units=64, batch_size=1024, obs_dims=[18, 18, 18], n=3,
+                               local_q=[False] * 3)
+    assert abs(bench.flops_critic_grad(s2, 0) / 1e6 - 95.4) < 0.1
+    assert abs(bench.bytes_critic_grad(s2, 0) - 863068) <= 4
+    assert abs(bench.bytes_actor_grad(s2, 0) / 1e6 - 0.500) < 0.005
+    assert abs(bench.flops_actor_grad(s2, 0) / 1e6 - 58.6) < 0.1
+    s5 = types.SimpleNamespace(num_units=128, batch_size=4096, obs_dims=[22, 22, 22, 22, 20, 20], n=6,
+                               local_q=[False] * 6)
+    assert abs(bench.flops_critic_grad(s5, 0) / 1e6 - 2009) < 2
+    assert abs(bench.bytes_critic_grad(s5, 0) / 1e6 - 6.40) < 0.01
+    assert bench.MARKER_KINDS == ("allreduce", "gather")
