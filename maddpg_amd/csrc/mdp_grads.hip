@@ -37,6 +37,12 @@
 #define MDP_GEN_THREADS 1024  // 16 waves: 4 per SIMD to cover the weight-chunk latency
 #endif
 
+#ifdef MDP_STAMPS
+// diagnostic: the layer work queue's units of workgroup 0 (critic kernel, first
+// pass): [unit][wave, layer << 8 | net, g, t_take, t_done] (s_memrealtime)
+__device__ unsigned long long g_q_trace[160][5];
+__device__ unsigned int g_q_n;
+#endif
 namespace {
 // Y[16][col tile nt] = act(X[16][K] @ W[K][N] + b), weights in 64-deep chunks, the next in flight
 template <bool RELU>
@@ -230,6 +236,9 @@ __device__ __forceinline__ void fwd_phase_l12(float* lds, int nj1, int nj2, int 
   struct It {
     int layer, net, g, c0;
     TileJob j;
+#ifdef MDP_STAMPS
+    unsigned long long t0;
+#endif
   };
   // next unit from the queue (one LDS atomic per unit, lane 0, broadcast)
   auto take = [&](It& it) -> bool {
@@ -244,6 +253,9 @@ __device__ __forceinline__ void fwd_phase_l12(float* lds, int nj1, int nj2, int 
     it.j = job(it.layer, jb);
     it.g = qq % ngr;
     it.c0 = it.j.k0;
+#ifdef MDP_STAMPS
+    it.t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     return true;
   };
   auto next = [&](It& it) -> bool {
@@ -285,6 +297,18 @@ __device__ __forceinline__ void fwd_phase_l12(float* lds, int nj1, int nj2, int 
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (it.layer == 0) lds_signal(cnt + it.net);
+#ifdef MDP_STAMPS
+      if (blockIdx.x == 0 && lane == 0) {
+        const unsigned q = atomicAdd(&g_q_n, 1u);
+        if (q < 160) {
+          g_q_trace[q][0] = threadIdx.x >> 6;
+          g_q_trace[q][1] = (unsigned long long)(it.layer << 8 | it.net);
+          g_q_trace[q][2] = it.g;
+          g_q_trace[q][3] = it.t0;
+          g_q_trace[q][4] = __builtin_amdgcn_s_memrealtime();
+        }
+      }
+#endif
     }
   };
   load(wa, ba, a);
@@ -1029,6 +1053,14 @@ hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipSt
 
 #ifdef MDP_STAMPS
 // diagnostic build: stamps of this translation unit's kernels (own code object)
+// the queue trace of the last critic launch (reset = 1: clear it)
+extern "C" int mdp_debug_q_trace(unsigned long long* out, int reset) {
+  if (reset) {
+    unsigned z = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_q_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_q_trace), sizeof(unsigned long long) * 160 * 5) == hipSuccess ? 0 : -1;
+}
 extern "C" int mdp_debug_stamps(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mdp_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
 }
