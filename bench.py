@@ -293,6 +293,9 @@ def main():
     ap.add_argument("--allow-torch-dist", action="store_true",
                     help="N>1: accept the torch.distributed fallback exchange (~14x slower per round) when "
                          "neither the direct xGMI exchange nor the library's RCCL communicator came up")
+    ap.add_argument("--step-group", type=int, default=10,
+                    help="timed steps replayed as graphs of this many consecutive steps (mdp_train_steps; "
+                         "1: one graph per step)")
     ap.add_argument("--no-gather-stage", action="store_true",
                     help="skip the gather-only stage figure (SURVEY 8d, rank 0 at N=1)")
     args = ap.parse_args()
@@ -333,13 +336,22 @@ def main():
     r.synchronize()
 
     xgmi = world > 1 and getattr(r, "dp_kind", None) == "native-xgmi"
+    # the timed steps as graphs of step_group consecutive steps, captured here
+    # ahead of the timed region (the same launches as step-by-step graphs; one
+    # graph-launch boundary per group instead of per step)
+    groups = r.prepare_steps(args.steps, args.step_group) if (args.step_group > 1 and not args.rollout_only) \
+        else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rounds = 0
-    for _ in range(args.steps):
-        rounds += one_step()
+    if groups:
+        for g in groups:
+            rounds += r.steps(g)
+    else:
+        for _ in range(args.steps):
+            rounds += one_step()
     torch.cuda.synchronize()
     dt_local = time.perf_counter() - t0     # this rank's own finish, before the closing barrier
     if world > 1:
@@ -560,7 +572,8 @@ def main():
                                       if any(eng.local_q) else ""),
                        "scenario": args.scenario, "num_envs_per_gpu": args.num_envs,
                        "global_batch": args.batch_size * world, "parallelism": f"dp{world}",
-                       "mode": "rollout-only" if args.rollout_only else args.update_mode},
+                       "mode": "rollout-only" if args.rollout_only else args.update_mode,
+                       "step_graph_group": args.step_group if groups else 1},
             "trainer_updates_per_sec": round(updates / dt, 3),
             "rounds_per_sec": round(rounds / dt, 3),
             "rollout_only_env_steps_per_sec": round(rollout_only, 3),

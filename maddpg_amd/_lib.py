@@ -119,6 +119,7 @@ SIGNATURES = {
     "mdp_dp_info": (ctypes.c_int, [_P, _I32P]),
     "mdp_dp_exchange_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), _I32]),
     "mdp_dp_exchange_stats_enable": (ctypes.c_int, [_P, _I32]),
+    "mdp_train_steps": (ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_int32), _I32]),
     "mdp_agent_update": (ctypes.c_int, [_P, _I32, ctypes.c_int64, _P, _P, ctypes.POINTER(ctypes.c_double)]),
     "mdp_ra_plan": (ctypes.c_int, [ctypes.POINTER(MdpConfig), _I32, _I32, _I32P]),
     "mdp_critic_grad": (ctypes.c_int, [_P, _I32, _P, _P]),

@@ -310,6 +310,8 @@ struct mdp_handle {
   hipGraphExec_t round_exec = nullptr;
   // mdp_train_step graphs (rollout + k rounds), one per k
   std::map<int, hipGraphExec_t> step_exec;
+  // mdp_train_steps graphs: several consecutive steps as one graph, keyed by their round counts
+  std::map<std::vector<int>, hipGraphExec_t> multi_exec;
   int eager_steps = 0;
   // native data parallelism (mdp_dp_init): RCCL communicator of this rank
   ncclComm_t comm = nullptr;
@@ -530,6 +532,14 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
     }
     if (apre) a.apre = h->apre;
     if (post_prev >= 0) a.cpre = h->cpre;
+#ifdef MDP_EXP_WARM_ICACHE  // timing only: an untimed launch of the same kernel first (warm instruction cache)
+    {
+      const MdpLaunchEv saved = mdp_launch_ev();
+      mdp_launch_ev() = MdpLaunchEv{};
+      HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
+      mdp_launch_ev() = saved;
+    }
+#endif
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
     return 0;
   }
@@ -580,6 +590,14 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
       a.cpre = h->cpre;
       lds = std::max(lds, lds_critic_pre_bytes(h->L.topo));
     }
+#ifdef MDP_EXP_WARM_ICACHE
+    {
+      const MdpLaunchEv saved = mdp_launch_ev();
+      mdp_launch_ev() = MdpLaunchEv{};
+      HIPCHK(h, mdp_launch_actor_grad_r(a, lds, h->stream));
+      mdp_launch_ev() = saved;
+    }
+#endif
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds, h->stream));
     return 0;
   }
@@ -1236,6 +1254,7 @@ int mdp_destroy(mdp_handle* h) {
   if (h->comm) (void)rccl().destroy(h->comm);
   xgmi_release(h);
   for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->multi_exec) (void)hipGraphExecDestroy(kv.second);
   if (h->round_graph) (void)hipGraphDestroy(h->round_graph);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -1629,7 +1648,9 @@ int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank
   h->dp_graphs = g && g[0] == '1';
   // drop graphs captured without the collectives
   for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->multi_exec) (void)hipGraphExecDestroy(kv.second);
   h->step_exec.clear();
+  h->multi_exec.clear();
   if (h->round_exec) {
     (void)hipGraphExecDestroy(h->round_exec);
     h->round_exec = nullptr;
@@ -1783,7 +1804,9 @@ int mdp_set_graphs(mdp_handle* h, int32_t on) {
 
 static void drop_graphs(mdp_handle* h) {
   for (auto& kv : h->step_exec) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->multi_exec) (void)hipGraphExecDestroy(kv.second);
   h->step_exec.clear();
+  h->multi_exec.clear();
   h->eager_steps = 0;
   if (h->round_exec) {
     (void)hipGraphExecDestroy(h->round_exec);
@@ -1992,6 +2015,74 @@ static int train_step_body(mdp_handle* h, int rounds) {
   }
   HIPCHK(h, hipGraphLaunch(it->second, h->stream));
   return 0;
+}
+
+// several consecutive training steps captured as ONE graph (keyed by their
+// round counts): the launches are exactly those of the steps one by one, but a
+// graph launch boundary costs ~6.7 us on the GPU clock against ~1.5-2 us for a
+// kernel boundary inside a graph (tools/step_boundary.py)
+static int multi_graph(mdp_handle* h, const std::vector<int>& ks, hipGraphExec_t* out) {
+  auto it = h->multi_exec.find(ks);
+  if (it != h->multi_exec.end()) {
+    *out = it->second;
+    return 0;
+  }
+  HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  h->capturing = true;
+  int rc = 0;
+  for (size_t i = 0; i < ks.size() && !rc; ++i) rc = step_launches(h, ks[i]);
+  h->capturing = false;
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(h->stream, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return fail(h, "hipStreamEndCapture", e);
+  hipGraphExec_t x = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (ei != hipSuccess) return fail(h, "hipGraphInstantiate", ei);
+  h->multi_exec.emplace(ks, x);
+  *out = x;
+  return 0;
+}
+
+int mdp_train_steps(mdp_handle* h, int32_t n, const int32_t* rounds, int32_t launch) {
+  if (need_env(h)) return -1;
+  if (n < 1 || n > 64 || !rounds) return fail(h, "mdp_train_steps: 1 <= n <= 64 steps");
+  std::vector<int> ks(rounds, rounds + n);
+  bool all_train = true;
+  for (int k : ks) {
+    if (k < 0 || k > 64) return fail(h, "mdp_train_steps: rounds must be in [0, 64]");
+    all_train = all_train && k > 0;
+  }
+  const bool no_graph = h->comm && !h->dp_graphs;
+  const bool graphable = h->graphs && !no_graph && !any_prof(h) && h->eager_steps >= 1 && all_train;
+  if (!launch) {  // capture and instantiate ahead of time (nothing runs)
+    hipGraphExec_t x = nullptr;
+    return graphable ? multi_graph(h, ks, &x) : 0;
+  }
+  if (!graphable) {
+    for (int k : ks) {
+      const int rc = mdp_train_step(h, k);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  const int64_t len0 = h->len, next0 = h->next;
+  for (int i = 0; i < n; ++i) advance_ring_mirror(h);
+  hipGraphExec_t x = nullptr;
+  int rc = multi_graph(h, ks, &x);
+  if (!rc) {
+    const hipError_t e = hipGraphLaunch(x, h->stream);
+    if (e != hipSuccess) rc = fail(h, "hipGraphLaunch", e);
+  }
+  if (rc) {
+    h->len = len0;
+    h->next = next0;
+  }
+  return rc;
 }
 
 int mdp_train_step(mdp_handle* h, int32_t rounds) {

@@ -409,6 +409,13 @@ class Engine:
         (mdp_train_step; single-GPU path)."""
         self._c("mdp_train_step", int(rounds))
 
+    def train_steps(self, rounds, launch=True):
+        """len(rounds) consecutive vector steps (step i: rollout + rounds[i] update
+        rounds) as ONE graph replay (mdp_train_steps); launch=False only
+        captures and instantiates that graph ahead of time."""
+        ks = (ctypes.c_int32 * len(rounds))(*[int(k) for k in rounds])
+        self._c("mdp_train_steps", len(rounds), ks, 1 if launch else 0)
+
     def dp_init(self, world, rank, uid=None):
         """Native data parallelism: join an RCCL communicator of `world` ranks
         (mdp_dp_init).  `uid` (128 bytes) comes from rank 0's dp_unique_id();

@@ -111,6 +111,47 @@ class VecRunner:
             self.train_round()
         return k
 
+    def plan(self, n, skip=0):
+        """the update rounds of vector steps skip .. skip + n - 1 from now (the
+        cadence of step()), or None when one of them would not train (replay
+        below the gate)"""
+        ks, t, ln = [], self.train_step, self.eng.buffer_len()
+        for i in range(skip + n):
+            ln = min(self.eng.capacity, ln + self.num_envs)
+            k = 0 if ln < self.gate else rounds_due(t, t + self.num_envs, self.train_every)
+            t += self.num_envs
+            if i < skip:
+                continue
+            if k == 0:
+                return None
+            ks.append(k)
+        return ks
+
+    def steps(self, n):
+        """n vector steps as one graph replay (mdp_train_steps) when every one of
+        them trains (single GPU or the native exchanges); otherwise step() n
+        times.  Returns the update rounds run."""
+        ks = self.plan(n) if (self.world_size == 1 or self.native_dp) else None
+        if ks is None:
+            return sum(self.step() for _ in range(n))
+        self.eng.train_steps(ks)
+        self.train_step += n * self.num_envs
+        self.rounds += sum(ks)
+        return sum(ks)
+
+    def prepare_steps(self, n, group):
+        """capture ahead of time the graphs steps(group) will replay over the next
+        n vector steps (nothing runs); returns the group sizes to call steps() with"""
+        sizes = [min(group, n - i) for i in range(0, n, group)]
+        if self.world_size == 1 or self.native_dp:
+            done = 0
+            for g in sizes:
+                ks = self.plan(g, skip=done)
+                if ks is not None:
+                    self.eng.train_steps(ks, launch=False)
+                done += g
+        return sizes
+
     def prefill(self):
         """vector steps without training until the replay gate opens (train.py warm-up)."""
         while self.eng.buffer_len() < self.gate:

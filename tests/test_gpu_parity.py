@@ -694,6 +694,44 @@ def test_train_step_graph_equals_step_then_rounds(monkeypatch, scenario, adv_pol
     np.testing.assert_array_equal(a.eng.get_rng_state(), b.eng.get_rng_state())
 
 
+@pytest.mark.parametrize("general", [False, True])
+def test_train_steps_group_graph_equals_step_graphs(monkeypatch, general):
+    """mdp_train_steps (several consecutive steps captured as ONE graph, captured
+    ahead of time with launch=0, then replayed) is the same work as the
+    steps one by one (one graph per step): bit-identical parameters, Adam
+    moments, replay ring, RNG stream and finished-episode count after two
+    groups (5 + 3 steps; the ring fills and wraps on the way, cap=3300)."""
+    from maddpg_amd.runner import VecRunner
+    if general:
+        monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
+
+    def make():
+        r = VecRunner("simple_spread", 64, batch_size=128, capacity=3300, seed=7, train_every=16)
+        r.prefill()
+        r.step()                          # the one eager training step
+        return r
+
+    a, b = make(), make()
+    sizes = a.prepare_steps(8, 5)
+    assert sizes == [5, 3]
+    ra = sum(a.steps(g) for g in sizes)
+    rb = sum(b.step() for _ in range(8))
+    assert ra == rb == 32 and a.train_step == b.train_step
+    a.eng.synchronize()
+    b.eng.synchronize()
+    for i in range(a.n):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_actor", "v_critic"):
+            pa, pb = a.eng.get_params(i, w), b.eng.get_params(i, w)
+            for key in pa:
+                np.testing.assert_array_equal(pa[key], pb[key])
+        for net in (0, 1):
+            np.testing.assert_array_equal(a.eng.get_beta_powers(i, net), b.eng.get_beta_powers(i, net))
+    np.testing.assert_array_equal(a.eng.replay_rows(0, 3300).cpu().numpy(), b.eng.replay_rows(0, 3300).cpu().numpy())
+    assert a.eng.buffer_len() == b.eng.buffer_len()
+    np.testing.assert_array_equal(a.eng.get_rng_state(), b.eng.get_rng_state())
+    assert a.episodes() == b.episodes()
+
+
 # ---------------------------------------------------- size-independent checks
 def test_full_size_index_stream_properties():
     """BASELINE S3-sized draw (1e6-row ring, 6 x 4096 indices): bit-exact vs
