@@ -293,7 +293,7 @@ def main():
     ap.add_argument("--allow-torch-dist", action="store_true",
                     help="N>1: accept the torch.distributed fallback exchange (~14x slower per round) when "
                          "neither the direct xGMI exchange nor the library's RCCL communicator came up")
-    ap.add_argument("--step-group", type=int, default=10,
+    ap.add_argument("--step-group", type=int, default=1,
                     help="timed steps replayed as graphs of this many consecutive steps (mdp_train_steps; "
                          "1: one graph per step)")
     ap.add_argument("--no-gather-stage", action="store_true",
