@@ -532,14 +532,6 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
     }
     if (apre) a.apre = h->apre;
     if (post_prev >= 0) a.cpre = h->cpre;
-#ifdef MDP_EXP_WARM_ICACHE  // timing only: an untimed launch of the same kernel first (warm instruction cache)
-    {
-      const MdpLaunchEv saved = mdp_launch_ev();
-      mdp_launch_ev() = MdpLaunchEv{};
-      HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
-      mdp_launch_ev() = saved;
-    }
-#endif
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
     return 0;
   }
@@ -590,14 +582,6 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
       a.cpre = h->cpre;
       lds = std::max(lds, lds_critic_pre_bytes(h->L.topo));
     }
-#ifdef MDP_EXP_WARM_ICACHE
-    {
-      const MdpLaunchEv saved = mdp_launch_ev();
-      mdp_launch_ev() = MdpLaunchEv{};
-      HIPCHK(h, mdp_launch_actor_grad_r(a, lds, h->stream));
-      mdp_launch_ev() = saved;
-    }
-#endif
     HIPCHK(h, mdp_launch_actor_grad_r(a, lds, h->stream));
     return 0;
   }
