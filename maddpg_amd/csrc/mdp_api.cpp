@@ -490,7 +490,8 @@ bool tp_fast(const mdp_handle* h);
 // partials / stats / TD targets and noise counter upd_ctr + agent (multi = 2
 // marks it; the general kernels take the agent from a.agent, not the grid)
 int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr,
-                   bool tp = false, bool apre = false, const float* u_act = nullptr, int post_prev = -1) {
+                   bool tp = false, bool apre = false, const float* u_act = nullptr, int post_prev = -1,
+                   int pf_n = 0) {
   CriticArgs a;
   a.apre = nullptr;
   a.u_act = u_act;
@@ -526,9 +527,9 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   }
   ProfScope p(h, MDP_K_CRITIC_GRAD);
   if (!tp && !h->general_grads && grads_r_ok(h->L.topo, agent)) {
-    if (pf_out) {
+    if (pf_out) {  // pf_n indices of the next round's draw (0: all n B of them)
       a.pf_out = pf_out;
-      a.pf_count = h->cfg.n_agents * h->cfg.batch_size;
+      a.pf_count = pf_n > 0 ? pf_n : h->cfg.n_agents * h->cfg.batch_size;
     }
     if (apre) a.apre = h->apre;
     if (post_prev >= 0) a.cpre = h->cpre;
@@ -820,6 +821,7 @@ bool critic_pre_ok(const mdp_handle* h, int p, int k) {
 struct DrawPieces {
   int32_t* out = nullptr;   // this agent's critic-step piece; the actor-step piece follows it
   int n_critic = 0, n_actor = 0;
+  int n_grad = 0;           // the critic-gradient launch's draw into pf_out (0: the whole next round)
 };
 
 int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, const float* u_act,
@@ -828,12 +830,12 @@ int do_update_dp(mdp_handle* h, int agent, const int32_t* idx, const float* u_tg
   const bool pre = actor_pre_ok(h, agent);
   int rc;
   if (h->p2p) {  // the exchange lives inside the optimizer launch: same 4 launches as one GPU
-    if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev))) return rc;
+    if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev, dp.n_grad))) return rc;
     if ((rc = do_reduce_apply(h, agent, 1, dp.out, dp.n_critic))) return rc;
     if ((rc = do_actor_grad(h, agent, idx, u_act, false, pre, pre_next, pre_idx))) return rc;
     return do_reduce_apply(h, agent, 0, dp.out ? dp.out + dp.n_critic : nullptr, dp.n_actor);
   }
-  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev, dp.n_grad))) return rc;
   if ((rc = do_reduce(h, agent, 1))) return rc;
   if ((rc = dp_allreduce(h, agent, 1))) return rc;
   if ((rc = do_apply(h, agent, 1, false, scale))) return rc;
@@ -856,7 +858,7 @@ int do_update(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, 
   int rc;
   const bool fused = h->fused_apply && reduce_apply_ok(h, agent, 0) && reduce_apply_ok(h, agent, 1);
   const bool pre = actor_pre_ok(h, agent);
-  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev))) return rc;
+  if ((rc = do_critic_grad(h, agent, idx, u_tgt, pf_out, false, pre, u_act, post_prev, dp.n_grad))) return rc;
   if (fused) {
     if ((rc = do_reduce_apply(h, agent, 1, dp.out, dp.n_critic))) return rc;
   } else {
@@ -1517,9 +1519,17 @@ static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nu
   if (carry_out) *carry_out = false;
   if (h->update_mode == 1) return do_round_tp(h, idx, nullptr, nullptr, pf_out);
   const int nb = n * B, piece = (nb + 2 * n - 1) / (2 * n);
+  // the next round's draw (pf_out) in per-agent pieces, agent i's B indices in
+  // agent i's critic launch -- the stream order of one n B draw (every launch
+  // continues the MT19937 state in Ctl) -- when every critic launch is a fast
+  // one; one n B draw in agent 0's launch made that launch the round's
+  // longest (rocprof 10.1 vs 9.2 us)
+  bool pieces = pf_out != nullptr && !h->general_grads;
+  for (int i = 0; i < n && pieces; ++i) pieces = grads_r_ok(h->L.topo, i);
   int rc = 0;
   for (int i = 0; i < n && !rc; ++i) {
     DrawPieces dp;
+    if (pieces) dp.n_grad = B;
     if (draw_out) {
       const int o = std::min(nb, 2 * i * piece);
       dp.out = draw_out + o;
@@ -1537,8 +1547,8 @@ static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nu
       pre_idx = next_idx;
       if (carry_out) *carry_out = true;
     }
-    rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, i == 0 ? pf_out : nullptr, post_prev, pre_next,
-                   pre_idx, dp);
+    int32_t* pf_i = pieces ? pf_out + (int64_t)i * B : (i == 0 ? pf_out : nullptr);
+    rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, pf_i, post_prev, pre_next, pre_idx, dp);
   }
   return rc;
 }
