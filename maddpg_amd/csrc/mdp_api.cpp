@@ -332,6 +332,7 @@ struct mdp_handle {
   // the xGMI batch only when its whole grid is co-resident (every chunk
   // workgroup spins on its peers' matching chunk); otherwise one launch per net
   bool rollout_draw = true;           // step_launches: first-round draw inside k_rollout
+  bool draw_ahead = true;             // step_launches: draws one agent ahead (MDP_DRAW_AHEAD=0: per round)
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
   uint64_t* xbuf = nullptr;
@@ -1133,6 +1134,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->fused_apply = !(u && u[0] == '1');
     const char* rd = getenv("MDP_ROLLOUT_DRAW");
     h->rollout_draw = !(rd && rd[0] == '0');
+    const char* da = getenv("MDP_DRAW_AHEAD");
+    h->draw_ahead = !(da && da[0] == '0');
     const char* ap = getenv("MDP_ACTOR_PRE");
     h->actor_pre = !(ap && ap[0] == '0');
     const char* cp = getenv("MDP_CRITIC_PRE");
@@ -1513,8 +1516,16 @@ int mdp_agent_update(mdp_handle* h, int32_t agent, int64_t t, const int32_t* idx
 // draw_out: the next round's n*B indices drawn in 2n pieces by the round's
 // optimizer launches (configurations without the fast critic kernel's
 // prefetch; only where every step is the one-launch fused kind)
+// ahead: the draw runs one agent ahead instead -- agent i's launches draw
+// agent i+1's B indices of THIS round into idx (which the caller then owns),
+// the last agent's the next round's agent 0 into pf_out (ahead 1: in the fast
+// critic launches) or draw_out (ahead 2: in the optimizer launches), if any:
+// the MT19937 stream order of the reference's per-agent make_index calls
+// (maddpg.py:173), with only agent 0's B of a step's first round left to the
+// rollout's draw workgroup
 static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nullptr, bool carry_in = false,
-                         const int32_t* next_idx = nullptr, bool* carry_out = nullptr, int32_t* draw_out = nullptr) {
+                         const int32_t* next_idx = nullptr, bool* carry_out = nullptr, int32_t* draw_out = nullptr,
+                         int ahead = 0) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   if (carry_out) *carry_out = false;
   if (h->update_mode == 1) return do_round_tp(h, idx, nullptr, nullptr, pf_out);
@@ -1524,13 +1535,20 @@ static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nu
   // continues the MT19937 state in Ctl) -- when every critic launch is a fast
   // one; one n B draw in agent 0's launch made that launch the round's
   // longest (rocprof 10.1 vs 9.2 us)
-  bool pieces = pf_out != nullptr && !h->general_grads;
-  for (int i = 0; i < n && pieces; ++i) pieces = grads_r_ok(h->L.topo, i);
+  bool pieces = ahead == 1 || (ahead == 0 && pf_out != nullptr && !h->general_grads);
+  for (int i = 0; i < n && pieces && ahead == 0; ++i) pieces = grads_r_ok(h->L.topo, i);
+  int32_t* cur = const_cast<int32_t*>(idx);
   int rc = 0;
   for (int i = 0; i < n && !rc; ++i) {
     DrawPieces dp;
     if (pieces) dp.n_grad = B;
-    if (draw_out) {
+    if (ahead == 2) {
+      dp.out = i + 1 < n ? cur + (int64_t)(i + 1) * B : draw_out;
+      if (dp.out) {
+        dp.n_critic = (B + 1) / 2;
+        dp.n_actor = B - dp.n_critic;
+      }
+    } else if (draw_out) {
       const int o = std::min(nb, 2 * i * piece);
       dp.out = draw_out + o;
       dp.n_critic = std::min(piece, nb - o);
@@ -1547,7 +1565,9 @@ static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nu
       pre_idx = next_idx;
       if (carry_out) *carry_out = true;
     }
-    int32_t* pf_i = pieces ? pf_out + (int64_t)i * B : (i == 0 ? pf_out : nullptr);
+    int32_t* pf_i = ahead == 1 ? (i + 1 < n ? cur + (int64_t)(i + 1) * B : pf_out)
+                    : pieces        ? pf_out + (int64_t)i * B
+                                    : (i == 0 ? pf_out : nullptr);
     rc = do_update(h, i, idx + (int64_t)i * B, nullptr, nullptr, pf_i, post_prev, pre_next, pre_idx, dp);
   }
   return rc;
@@ -1962,18 +1982,24 @@ int mdp_env_step_bench(mdp_handle* h, float* info_dev) {
 static int step_launches(mdp_handle* h, int rounds) {
   const int nb = h->cfg.n_agents * h->cfg.batch_size;
   int32_t* slot[2] = {h->index, h->index + nb};
+  const bool pf = prefetch_ok(h);
+  const bool ra_draw = !pf && h->update_mode == 0 && draw_in_ra_ok(h);
+  bool fast_all = !h->general_grads;
+  for (int i = 0; i < h->cfg.n_agents && fast_all; ++i) fast_all = grads_r_ok(h->L.topo, i);
+  // one agent ahead (round_updates): the step's first draw is agent 0's B only
+  const int ahead = !h->draw_ahead || h->update_mode != 0 ? 0 : (pf && fast_all) ? 1 : ra_draw ? 2 : 0;
+  const int first = ahead ? h->cfg.batch_size : nb;
   // the first round's draw rides in the rollout launch (MDP_ROLLOUT_DRAW=0: its own launch)
   const bool in_rollout = rounds > 0 && h->rollout_draw;
-  int rc = env_step_launch(h, nullptr, nullptr, nullptr, in_rollout ? slot[0] : nullptr, nb);
+  int rc = env_step_launch(h, nullptr, nullptr, nullptr, in_rollout ? slot[0] : nullptr, first);
   if (rc || rounds == 0) return rc;
-  const bool pf = prefetch_ok(h);
-  if (!in_rollout && (rc = launch_make_index(h, nb, slot[0]))) return rc;
+  if (!in_rollout && (rc = launch_make_index(h, first, slot[0]))) return rc;
   bool carry = false;
-  const bool ra_draw = !pf && h->update_mode == 0 && draw_in_ra_ok(h);
   for (int r = 0; r < rounds && !rc; ++r) {
     const bool more = r + 1 < rounds;
-    int32_t* next = (more && pf) ? slot[(r + 1) & 1] : nullptr;  // drawn in agent 0's critic launch
-    rc = round_updates(h, slot[r & 1], next, carry, next, &carry, (more && ra_draw) ? slot[(r + 1) & 1] : nullptr);
+    int32_t* next = (more && pf) ? slot[(r + 1) & 1] : nullptr;  // drawn in the critic launches
+    rc = round_updates(h, slot[r & 1], next, carry, next, &carry, (more && ra_draw) ? slot[(r + 1) & 1] : nullptr,
+                       ahead);
     if (!rc && more && !pf && !ra_draw) rc = launch_make_index(h, nb, slot[(r + 1) & 1]);
   }
   return rc;

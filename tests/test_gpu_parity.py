@@ -656,9 +656,10 @@ def test_rollout_policy_actions_match_oracle():
 ])
 def test_train_step_graph_equals_step_then_rounds(monkeypatch, scenario, adv_policy, cap, general):
     """mdp_train_step(k) (rollout + k rounds replayed as one graph; the first
-    round's indices drawn by an extra rollout workgroup, the later rounds' by
-    the fast critic kernel -- or, on the general kernels, in pieces by the
-    optimizer launches; the critic split carried from a round's last actor
+    round's agent-0 indices drawn by an extra rollout workgroup, every later
+    agent's B indices one agent ahead -- by the previous agent's fast critic
+    kernel or, on the general kernels, in two pieces by its optimizer
+    launches; the critic split carried from a round's last actor
     launch into the next round's agent 0) is the same work as env_step + k x
     update_round (eager rounds, no carry): bit-identical state and RNG stream
     after 4 steps.  cap=3300: the ring fills during the steps (draws against

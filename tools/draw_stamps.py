@@ -1,6 +1,6 @@
-"""Diagnostic: duration of the index-draw workgroup of k_rollout (the first
-update round's n*B indices, block 0 of the training step's rollout) from the
--DMDP_STAMPS build, S2 or (arg tag6) S5:
+"""Diagnostic: the index-draw workgroup of k_rollout (the step's first draw)
+against env workgroup 0 of the same launch, on the s_memrealtime clock, from
+the -DMDP_STAMPS build, S2 or (arg tag6) S5:
     make -C maddpg_amd/csrc stamps
     MDP_LIB=maddpg_amd/libmaddpg_hip_stamps.so python tools/draw_stamps.py [tag6]"""
 import ctypes
@@ -32,4 +32,7 @@ for _ in range(3):
     eng.synchronize()
     fn(buf, 64)
     st = np.array(buf[:], dtype=np.int64)
-    print(f"draw workgroup: {eng.n} x {eng.batch_size} indices in {(st[49] - st[48]) * 10 / 1000:.2f} us")
+    t0 = min(st[40], st[48])
+    us = lambda i: (st[i] - t0) * 10 / 1000  # noqa: E731
+    print(f"draw workgroup {us(48):6.2f} .. {us(49):6.2f} us ({us(49) - us(48):6.2f});"
+          f"  env workgroup 0 {us(40):6.2f} .. {us(47):6.2f} us ({us(47) - us(40):6.2f})")
