@@ -51,6 +51,58 @@ __global__ void k_read(const float* __restrict__ slab, int nwg, int64_t stride_w
   }
 }
 
+// the chunk's partials split over S workgroups: workgroup b reads part
+// b % S (partials [part nwg / S, (part + 1) nwg / S)) of chunk b / S
+template <int G>
+__global__ void k_read_split(const float* __restrict__ slab, int nwg, int64_t stride_w, int S, float* out) {
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6, c = blockIdx.x / S, part = blockIdx.x % S;
+  const float* base = slab + (int64_t)c * 256 + 4 * lane;
+  const int w_lo = part * nwg / S, w_hi = (part + 1) * nwg / S;
+  f32x4 v[16];
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int w0 = w_lo + g; w0 < w_hi; w0 += 16 * G) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int w = min(w0 + G * k, w_hi - 1);
+      v[k] = *reinterpret_cast<const f32x4*>(base + (int64_t)w * stride_w);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (w0 + G * k < w_hi) s += v[k];
+  }
+  __shared__ f32x4 red[G][64];
+  red[g][lane] = s;
+  __syncthreads();
+  if (g == 0) {
+    for (int q = 1; q < G; ++q) s += red[q][lane];
+    *reinterpret_cast<f32x4*>(out + (int64_t)blockIdx.x * 256 + 4 * lane) = s;
+  }
+}
+
+template <int G>
+static float run_split(int nchunk, int nwg, int S, int reps) {
+  const int64_t P = (int64_t)nchunk * 256;
+  float *slab, *out;
+  (void)hipMalloc(&slab, sizeof(float) * P * nwg);
+  (void)hipMalloc(&out, sizeof(float) * P * S);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  float tot = 0.f;
+  for (int r = 0; r < reps; ++r) {
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, slab, P * nwg);
+    hipExtLaunchKernelGGL(k_read_split<G>, dim3(nchunk * S), dim3(64 * G), 0, 0, a, b, 0u, (const float*)slab, nwg,
+                          P, S, out);
+    (void)hipEventSynchronize(b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    if (r > 0) tot += ms;
+  }
+  (void)hipFree(slab);
+  (void)hipFree(out);
+  return tot / (reps - 1) * 1e3f;
+}
+
 template <int G>
 static float run(int nchunk, int nwg, int cmajor, int reps) {
   const int64_t P = (int64_t)nchunk * 256;
@@ -85,5 +137,15 @@ int main() {
          run<16>(145, 256, 0, reps), run<16>(145, 256, 1, reps));
   printf("S5 actor (79 chunks x 256 partials, 16 waves): wg-major %.2f us, chunk-major %.2f us\n",
          run<16>(79, 256, 0, reps), run<16>(79, 256, 1, reps));
+  // the fan-in split over S workgroups per chunk (no combine): does reading
+  // from more CUs shorten the read?
+  printf("S5 critic split: S1 G16 %.2f  S2 G16 %.2f  S2 G8 %.2f  S4 G4 %.2f  S4 G8 %.2f us\n",
+         run_split<16>(145, 256, 1, reps), run_split<16>(145, 256, 2, reps), run_split<8>(145, 256, 2, reps),
+         run_split<4>(145, 256, 4, reps), run_split<8>(145, 256, 4, reps));
+  printf("S5 actor split:  S1 G16 %.2f  S2 G16 %.2f  S2 G8 %.2f  S4 G4 %.2f  S4 G8 %.2f us\n",
+         run_split<16>(79, 256, 1, reps), run_split<16>(79, 256, 2, reps), run_split<8>(79, 256, 2, reps),
+         run_split<4>(79, 256, 4, reps), run_split<8>(79, 256, 4, reps));
+  printf("S2 critic split: S1 G4 %.2f  S2 G4 %.2f  S2 G2 %.2f  S4 G1 %.2f us\n", run_split<4>(35, 64, 1, reps),
+         run_split<4>(35, 64, 2, reps), run_split<2>(35, 64, 2, reps), run_split<1>(35, 64, 4, reps));
   return 0;
 }
