@@ -1,7 +1,7 @@
 #!/bin/bash
 # One-GPU bench lines for every BASELINE.json config (run on a GPU box via gpurun):
 #   gpurun --timeout 900 -- 'bash tools/bench_configs.sh r01e'
-# configs[1] spread E=1024 (the default bench), configs[2]'s per-GPU size (E=4096),
+# configs[0] simple N=1 with one env (the reference's own CPU case, on the GPU), configs[1] spread E=1024 (the default bench), configs[2]'s per-GPU size (E=4096),
 # configs[3] adversary 1 adv (ddpg) + 2 good (maddpg), E=4096, configs[4] tag N=6
 # (4 adv + 2 good), H=128, B=4096.  Stops at the first failure.
 set -e
@@ -9,6 +9,7 @@ TAG=${1:-cfg}
 O=gpurun_out/$TAG/configs
 mkdir -p $O
 B="python3 bench.py --no-cpu-baseline --no-gather-stage --no-configs2 --steps 20 --warmup 3"
+timeout -k 10 240 $B --steps 500 --scenario simple --num-agents 1 --num-envs 1 > $O/s1_simple_e1.json 2> $O/s1.err
 timeout -k 10 240 $B > $O/s2_spread_e1024.json 2> $O/s2.err
 timeout -k 10 240 $B --num-envs 4096 > $O/s3_spread_e4096.json 2> $O/s3.err
 timeout -k 10 240 $B --scenario simple_adversary --num-envs 4096 --num-adversaries 1 --adv-policy ddpg \
