@@ -696,6 +696,37 @@ def test_train_step_graph_equals_step_then_rounds(monkeypatch, scenario, adv_pol
 
 
 @pytest.mark.parametrize("general", [False, True])
+def test_draw_ahead_equals_per_round_draw(monkeypatch, general):
+    """The index draw one agent ahead (MDP_DRAW_AHEAD, default on: the rollout
+    draws agent 0's B, every agent's launches the next agent's) is the same MT19937
+    stream as one n*B draw per round (MDP_DRAW_AHEAD=0): bit-identical
+    parameters, replay ring and RNG state after 4 training steps of 4 rounds,
+    on the fast kernels and on the general ones (draw pieces in the optimizer
+    launches)."""
+    from maddpg_amd.runner import VecRunner
+    if general:
+        monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
+
+    def run(ahead):
+        monkeypatch.setenv("MDP_DRAW_AHEAD", ahead)
+        r = VecRunner("simple_spread", 64, batch_size=128, capacity=20000, seed=5, train_every=16)
+        r.prefill()
+        for _ in range(4):
+            assert r.step() == 4
+        r.eng.synchronize()
+        return r
+
+    a, b = run("1"), run("0")
+    for i in range(a.n):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_critic", "v_actor"):
+            pa, pb = a.eng.get_params(i, w), b.eng.get_params(i, w)
+            for key in pa:
+                np.testing.assert_array_equal(pa[key], pb[key])
+    np.testing.assert_array_equal(a.eng.replay_rows(0, 2000).cpu().numpy(), b.eng.replay_rows(0, 2000).cpu().numpy())
+    np.testing.assert_array_equal(a.eng.get_rng_state(), b.eng.get_rng_state())
+
+
+@pytest.mark.parametrize("general", [False, True])
 def test_train_steps_group_graph_equals_step_graphs(monkeypatch, general):
     """mdp_train_steps (several consecutive steps captured as ONE graph, captured
     ahead of time with launch=0, then replayed) is the same work as the
