@@ -433,6 +433,27 @@ __device__ __forceinline__ void fwd_tile_pf(const float* X, int ldx, int k0, int
     Y[(kq * 4 + i) * ldy + col] = v;
   }
 }
+// mfma_chunk with the columns [z_lo, z_hi) of A read as zero (the actor
+// step's critic layer 1 before its a_i input exists)
+__device__ __forceinline__ f32x4 mfma_chunk_zc(f32x4 acc, const float (&w)[MDP_KC], const float* A, int lda, int r,
+                                               int c0, int K, int kq, int z_lo, int z_hi) {
+  const int kmax = K > 0 ? K - 1 : 0;
+  float x[MDP_KC];
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    const int k = c0 + 4 * s + kq;
+    const float v = A[r * lda + min(k, kmax)];
+    x[s] = (k < K && (k < z_lo || k >= z_hi)) ? v : 0.f;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < MDP_KC; ++s) {
+    if (c0 + 4 * s < K)  // wave-uniform
+      acc = MDP_MFMA(x[s], w[s], acc);
+  }
+  return acc;
+}
+
 // dX tile nt = (dY[16][N] @ W^T) masked by Hin > 0 (N a multiple of 64), first
 // chunk of W^T in wa (pf_load_t); contiguous transposed fragments (load_wchunk_tc)
 __device__ __forceinline__ void dgrad_tile_relu_pf(const float* dY, int ldy, int N, const float* __restrict__ W,
@@ -842,8 +863,24 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
 
   float pf[MDP_KC];  // this wave's next layer chunk, issued ahead (wave < NT)
   f32x4 pft[4];      // the next transposed (backward) chunk, issued ahead
+  // Critic layer 1 beside the actor forward (par, a MADDPG critic at H <= 128):
+  // its input is the replay row prefix except the a_i columns, which the
+  // Gumbel sample fills only after the actor head.  Waves NT .. 2 NT - 1 (idle
+  // during the single-net actor layers) run tile wave - NT of it over the row
+  // with a_i read as zero, one 64-deep weight chunk per phase of the actor
+  // forward (actor L1, actor L2, head + Gumbel), then add the a_i k-steps from
+  // the sample: the 3.8 us critic layer-1 phase (S5, stamped) becomes a
+  // two-k-step phase.  (The MFMA k order differs from one chain over the row:
+  // a_i's k-steps come last.)
+  constexpr bool kPar = 2 * NT <= MDP_GEN_THREADS / 64;
+  const bool par = kPar && !lq && ag.a_in_off + MDP_ACT_DIM <= cin;
+  const bool pw = par && wave >= NT && wave < 2 * NT;  // a partial wave (uniform)
+  const int a_lo = ag.a_in_off, a4 = a_lo & ~3;
+  f32x4 pacc = {0.f, 0.f, 0.f, 0.f};
+  float paw[2] = {0.f, 0.f};  // W1c rows a4 + 4 s + kq of this lane's column (the a_i k-steps)
   MDP_STAMP(32);
   if (wave < NT) pf_load(pf, P + na.t[0].off, H, wave, 0, ag.obs_dim);
+  if (pw) pf_load(pf, P + nc.t[0].off, H, wave - NT, 0, cin);
   gather_rows16(a.replay, T.row_stride, a.idx, r0, nvalid, rowbuf, ldr);
   for (int e = tid; e < MDP_ACT_DIM * H; e += blockDim.x) w1ai[e] = P[nc.t[0].off + (int64_t)ag.a_in_off * H + e];
   __syncthreads();
@@ -854,11 +891,18 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
                       ldh, wave, pf);
     pf_load(pf, P + na.t[2].off, H, wave, 0, H);
   }
-  // critic input with act_input_n[i] = the sample (maddpg.py:48-52): the replay part now
-  for (int e = tid; e < MDP_R * cin; e += blockDim.x) {
-    const int r = e / cin, c = e - r * cin;
-    const int src = lq ? (c < ag.obs_dim ? ag.obs_off + c : ag.act_off + c - ag.obs_dim) : c;
-    x[r * ldc + c] = rowbuf[r * ldr + src];
+  const int pcol = (wave - NT) * 16 + (lane & 15);  // the partial wave's column
+  if (pw) {
+    const float* W1c = P + nc.t[0].off;
+    pacc = mfma_chunk_zc(pacc, pf, rowbuf, ldr, lane & 15, 0, cin, lane >> 4, a_lo, a_lo + MDP_ACT_DIM);
+    if (4 * MDP_KC < cin) load_wchunk(pf, W1c, H, pcol, 4 * MDP_KC, cin, lane >> 4);
+  } else if (!par) {
+    // critic input with act_input_n[i] = the sample (maddpg.py:48-52): the replay part now
+    for (int e = tid; e < MDP_R * cin; e += blockDim.x) {
+      const int r = e / cin, c = e - r * cin;
+      const int src = lq ? (c < ag.obs_dim ? ag.obs_off + c : ag.act_off + c - ag.obs_dim) : c;
+      x[r * ldc + c] = rowbuf[r * ldr + src];
+    }
   }
   __syncthreads();
   MDP_STAMP(34);
@@ -868,7 +912,12 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   if (H / 4 <= 32 && wave == 0) head_load<HKS>(hw, hb, P + na.t[4].off, P + na.t[5].off, MDP_ACT_DIM);
   if (wave < NT) {
     fwd_tile_pf<true>(h1a, ldh, 0, H, P + na.t[2].off, P + na.t[3].off, H, nullptr, 0, h2a, ldh, wave, pf);
-    pf_load(pf, P + nc.t[0].off, H, wave, 0, cin);
+    if (par) pf_load(pf, P + nc.t[2].off, H, wave, 0, H);  // critic L2 follows the a_i step
+    else pf_load(pf, P + nc.t[0].off, H, wave, 0, cin);
+  } else if (pw && 4 * MDP_KC < cin) {
+    const float* W1c = P + nc.t[0].off;
+    pacc = mfma_chunk_zc(pacc, pf, rowbuf, ldr, lane & 15, 4 * MDP_KC, cin, lane >> 4, a_lo, a_lo + MDP_ACT_DIM);
+    if (8 * MDP_KC < cin) load_wchunk(pf, W1c, H, pcol, 8 * MDP_KC, cin, lane >> 4);
   }
   __syncthreads();
   MDP_STAMP(35);
@@ -885,13 +934,35 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
         uniforms5(a.seed, (uint32_t)((a.agent << 8) | 0x80), ctr, (uint32_t)(r0 + lane), u);
       }
       gumbel_softmax5(lg + lane * 8, u, av + lane * 8);
-      for (int k = 0; k < MDP_ACT_DIM; ++k) x[lane * ldc + ag.a_in_off + k] = av[lane * 8 + k];
+      if (!par)
+        for (int k = 0; k < MDP_ACT_DIM; ++k) x[lane * ldc + ag.a_in_off + k] = av[lane * 8 + k];
     }
+  } else if (pw) {
+    const float* W1c = P + nc.t[0].off;
+    for (int c0 = 8 * MDP_KC; c0 < cin; c0 += 4 * MDP_KC) {  // the rest of the row (cin > 128)
+      pacc = mfma_chunk_zc(pacc, pf, rowbuf, ldr, lane & 15, c0, cin, lane >> 4, a_lo, a_lo + MDP_ACT_DIM);
+      if (c0 + 4 * MDP_KC < cin) load_wchunk(pf, W1c, H, pcol, c0 + 4 * MDP_KC, cin, lane >> 4);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) paw[q] = W1c[min(a4 + 4 * q + (lane >> 4), cin - 1) * H + pcol];
   }
   __syncthreads();
   MDP_STAMP(36);
   // critic (post-step weights) forward
-  if (wave < NT) {
+  if (par) {
+    if (pw) {  // + the a_i k-steps (rows a4 .. a4 + 7 of W1c; a_i's columns from the sample) + b1, ReLU
+      const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int k = a4 + 4 * q + kq;
+        const float xa = (k >= a_lo && k < a_lo + MDP_ACT_DIM) ? av[r * 8 + (k - a_lo)] : 0.f;
+        if (a4 + 4 * q < cin) pacc = MDP_MFMA(xa, paw[q], pacc);
+      }
+      const float bias = P[nc.t[1].off + pcol];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h1c[(kq * 4 + i) * ldh + pcol] = fmaxf(pacc[i] + bias, 0.f);
+    }
+  } else if (wave < NT) {
     fwd_tile_pf<true, true>(x, ldc, 0, cin, P + nc.t[0].off, P + nc.t[1].off, H, nullptr, 0, h1c, ldh, wave, pf);
     pf_load(pf, P + nc.t[2].off, H, wave, 0, H);
   }
