@@ -11,6 +11,7 @@ ranks) with everything resident in HBM.
 
     python bench.py                        # N=1, E=1024 (BASELINE configs[1])
     torchrun --nproc-per-node N bench.py --gpus N
+    python bench.py --gpus N               # launches the N ranks itself (torchrun as a child)
 """
 import argparse
 import json
@@ -135,43 +136,63 @@ def roofline_for(kind, eng, ms_avg):
             "algorithmic_per_launch": by, "avg_launch_ms": ms_avg}
 
 
-def gather_stage(obs_dims, sizes=(1024, 1 << 16, 1 << 20, 1 << 22), iters=20, capacity=1 << 20):
+MALL_BYTES = 256 << 20          # MI355X_MICROARCH.md: 256 MB Infinity Cache (MALL) in front of HBM
+HBM_ACHIEVABLE_GBS = 6290.0     # MI355X_MICROARCH.md: measured achievable HBM read+write rate
+
+
+def gather_stage(obs_dims, sizes=(1024, 1 << 16, 1 << 20, 1 << 22), iters=12, capacity=1 << 22):
     """SURVEY 8d's gather-only stage (replay_buffer.py:34-44 sample_index /
     _encode_sample, the HBM-roofline part of the north_star's fused
     sample+gather): k_gather_rows through mdp_sample_rows on uniform indices
-    over a full 2^20-row ring, at the training batch and at bandwidth-bound
-    row counts.  Algorithmic bytes per launch = B*row (read) + 4B (indices)
-    + B*row (the gathered rows written out; inside the gradient kernels they
-    go to LDS instead).  Duration: a HIP event pair around every launch on the
-    engine stream (mdp_prof_*, the empty pair's cost subtracted), so host
-    issue gaps between small launches do not count."""
+    over a full 2^22-row ring (2.2 GB at S2's 528-B rows, 8.7x the 256 MB
+    Infinity Cache), at the training batch and at bandwidth-bound row counts.
+    Every timed launch draws FRESH indices (its own index tensor, all drawn
+    before the timed launches), so no launch re-reads rows an earlier launch
+    left in the MALL; the written rows rotate over two output buffers.
+    Algorithmic bytes per launch = B*row (read) + 4B (indices) + B*row (the
+    gathered rows written out; inside the gradient kernels they go to LDS
+    instead).  Duration: a HIP event pair around every launch on the engine
+    stream (mdp_prof_*, the empty pair's cost subtracted), so host issue gaps
+    between small launches do not count.  `bound` per size: "hbm" when the
+    ring the indices range over is larger than the MALL (a random row hits it
+    with probability ~MALL/ring), "latency" for the training batch (a few
+    microseconds per launch: the dispatch and one row round trip bound it)."""
     from maddpg_amd.engine import Engine
     eng = Engine(obs_dims, batch_size=1024, capacity=capacity)
     eng.set_ring(capacity, 0)
     row_b = eng.row_stride * 4
+    ring_b = capacity * row_b
     ev = event_overhead_ms(eng.stream)
     res = []
     for B in sizes:
-        idx = torch.randint(0, capacity, (B,), dtype=torch.int32, device=eng.device)
-        out = torch.empty((B, eng.row_stride), dtype=torch.float32, device=eng.device)
+        gen = torch.Generator(device=eng.device)
+        gen.manual_seed(B)
+        # one index set per launch: iters timed + 2 warm-up
+        idxs = [torch.randint(0, capacity, (B,), dtype=torch.int32, device=eng.device, generator=gen)
+                for _ in range(iters + 2)]
+        outs = [torch.empty((B, eng.row_stride), dtype=torch.float32, device=eng.device) for _ in range(2)]
         torch.cuda.synchronize()
-        for _ in range(3):
-            eng.sample_rows(idx, out)
+        for k in range(2):
+            eng.sample_rows(idxs[k], outs[k & 1])
+        eng.synchronize()
         eng.prof_enable("gather", True)
-        for _ in range(iters):
-            eng.sample_rows(idx, out)
+        for k in range(iters):
+            eng.sample_rows(idxs[2 + k], outs[k & 1])
         eng.synchronize()
         ms_tot, n = eng.prof_read("gather")
         eng.prof_enable("gather", False)
         ms = max(ms_tot / n - ev, 1e-6)
         by = 2 * B * row_b + 4 * B
         gbs = by / (ms * 1e-3) / 1e9
+        bound = "latency" if B * row_b < (8 << 20) else ("hbm" if ring_b > 4 * MALL_BYTES else "cache")
         res.append({"rows": B, "bytes_per_launch": by, "avg_launch_ms": round(ms, 5), "achieved": round(gbs, 1),
-                    "frac": round(gbs / HBM_PEAK_GBS, 4)})
-        del idx, out
+                    "frac": round(gbs / HBM_PEAK_GBS, 4), "frac_of_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
+                    "bound": bound, "fresh_indices_per_launch": True})
+        del idxs, outs
     eng.close()
-    return {"bound": "hbm", "kernel": "k_gather_rows", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-            "row_bytes": row_b, "ring_rows": capacity, "sizes": res}
+    return {"kernel": "k_gather_rows", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achievable": HBM_ACHIEVABLE_GBS,
+            "row_bytes": row_b, "ring_rows": capacity, "ring_bytes": ring_b, "mall_bytes": MALL_BYTES,
+            "expected_mall_hit_share": round(min(1.0, MALL_BYTES / ring_b), 4), "sizes": res}
 
 
 def event_overhead_ms(stream, pairs=64):
@@ -188,6 +209,15 @@ def event_overhead_ms(stream, pairs=64):
     return ts[len(ts) // 2]
 
 
+def lib_sha256():
+    """first 16 hex digits of the sha256 of the library this process loads: ties a
+    committed rocprof summary (profiles/pmc_traffic.json `_lib_sha256`) to the
+    build it measured"""
+    import hashlib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_pmc(kernel, config_key):
     """the committed rocprofv3 PMC summary of `kernel` (profiles/pmc_traffic.json, written by
     tools/profile_summary.py): per-launch HBM bytes and the MFMA busy fraction."""
@@ -199,6 +229,8 @@ def load_pmc(kernel, config_key):
         out = dict(cfg.get(kernel) or {})
         if out and cfg.get("_source"):
             out["_source"] = "profiles/" + cfg["_source"]
+        if out:
+            out["_lib_sha256"] = cfg.get("_lib_sha256")
         return out
     except Exception:
         return {}
@@ -263,6 +295,41 @@ def configs2_per_gpu(args, steps=12, warmup=3):
     return out
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch_plan(gpus, environ, argv, port=None):
+    """How `bench.py --gpus N` becomes N ranks (pure host logic, tested on CPU).
+
+    * WORLD_SIZE set (torchrun / the driver's launch): it must equal --gpus,
+      else SystemExit(2) -- a line measured on another world size would be
+      reported under the wrong N;
+    * WORLD_SIZE unset and N > 1: the torchrun command that starts N fresh rank
+      processes of this script (one per GPU, rendezvous on 127.0.0.1), to run
+      as a child process before this one makes any GPU call;
+    * otherwise None: run here as the single rank."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            print(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}; refusing to report a {ws}-rank run as "
+                  f"n_gpus={gpus}", file=sys.stderr)
+            raise SystemExit(2)
+        return None
+    if gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port or _free_port()),
+            os.path.join(ROOT, "bench.py")] + list(argv)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,11 +365,23 @@ def main():
                          "1: one graph per step)")
     ap.add_argument("--no-gather-stage", action="store_true",
                     help="skip the gather-only stage figure (SURVEY 8d, rank 0 at N=1)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="print this rank's (rank, world, local rank) as JSON and exit before any GPU call "
+                         "(tests the --gpus N launch on a CPU host)")
     args = ap.parse_args()
 
+    # --gpus N is a contract: N ranks or no line at all.  Without torchrun's
+    # environment the bench launches the N rank processes itself (fresh
+    # children, before this process touches the GPU) and exits with their
+    # status; a WORLD_SIZE that disagrees with --gpus is an error.
+    plan = rank_launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if plan is not None:
+        sys.exit(subprocess.run(plan, cwd=ROOT).returncode)
+    if args.launch_check:
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "gpus": args.gpus}))
+        return
     world, rank, local = init_process_group_from_env()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if args.num_envs is None:   # BASELINE configs[1] on one GPU, configs[2] across GPUs
         args.num_envs = 1024 if world == 1 else 4096
     torch.cuda.set_device(local)
@@ -502,6 +581,7 @@ def main():
                           "(hipExtLaunchKernel) in an eager pass of the same workload; the pair's two "
                           "launch durations summed")
         roof["launches_timed"] = launches
+    lib_hash = lib_sha256()
     cfg_key = f"{args.scenario}_E{args.num_envs}_B{args.batch_size}_H{args.num_units}"
     if args.num_agents is not None:
         cfg_key += f"_N{args.num_agents}"
@@ -514,6 +594,7 @@ def main():
         if all(p.get("avg_ns") for p in parts):
             pmc["avg_ns"] = sum(p["avg_ns"] for p in parts)
             pmc["_source"] = parts[0].get("_source")
+            pmc["_lib_sha256"] = parts[0].get("_lib_sha256")
             if all(p.get("mfma_busy_frac") is not None for p in parts):
                 pmc["mfma_busy_frac"] = sum(p["mfma_busy_frac"] * p["avg_ns"] for p in parts) / pmc["avg_ns"]
     elif roof is not None:
@@ -525,25 +606,30 @@ def main():
             roof["mfma_busy_frac_rocprof"] = round(pmc["mfma_busy_frac"], 5)
         if pmc.get("avg_ns"):
             # the committed rocprofv3 --kernel-trace --stats average of the same kernel and
-            # workload (profiles/, mostly graph-replayed launches) is the headline duration; the
-            # live packet-event figure (eager launches of the kernel pass) is kept beside it and
-            # must agree: eager launches run ~3-5 % shorter than graph-replayed ones (the trace
-            # shows the same split), so a gap beyond 10 % means the profile is stale -> live
+            # workload (profiles/, mostly graph-replayed launches) is the headline duration ONLY
+            # when that profile measured this very library (same sha256); otherwise the live
+            # packet-event figure (eager launches of the kernel pass) is the headline and the
+            # stale profile is reported beside it
             live_ms = roof["avg_launch_ms"]
             prof_ms = pmc["avg_ns"] * 1e-6
             roof["rocprof_avg_launch_ms"] = round(prof_ms, 6)
+            roof["rocprof_lib_sha256"] = pmc.get("_lib_sha256")
             roof["live_avg_launch_ms"] = live_ms
             roof["live_achieved"] = roof["achieved"]
             roof["live_frac"] = roof["frac"]
             roof["live_vs_rocprof_duration"] = round(live_ms / prof_ms, 4)
-            if abs(live_ms / prof_ms - 1.0) <= 0.10:
+            if pmc.get("_lib_sha256") and pmc.get("_lib_sha256") == lib_hash:
                 scale = live_ms / prof_ms
                 roof["avg_launch_ms"] = prof_ms
                 roof["achieved"] = round(roof["achieved"] * scale, 4)
                 roof["frac"] = round(roof["frac"] * scale, 6)
-                roof["duration_source"] = f"rocprofv3 --kernel-trace --stats average ({pmc.get('_source', 'profiles')})"
+                roof["duration_source"] = (f"rocprofv3 --kernel-trace --stats average ({pmc.get('_source', 'profiles')}, "
+                                           f"library sha256 {lib_hash}, the one this run loaded)")
             else:
-                roof["duration_source"] = "live packet events (the committed rocprof summary is stale: >10 % apart)"
+                roof["duration_source"] = (f"live packet events (the committed rocprof summary measured library "
+                                           f"{pmc.get('_lib_sha256')}, this run loaded {lib_hash})")
+        else:
+            roof["duration_source"] = "live packet events (no committed rocprof summary for this workload)"
         if roof.get("traffic") and roof.get("algorithmic_bytes_per_launch"):
             # counted HBM bytes (2*FETCH + WRITE) over the algorithmic bytes: the re-read /
             # write-back excess of the launch (partial-gradient slabs, hand-off blocks, weights per XCD)
@@ -552,6 +638,7 @@ def main():
             roof["pmc_source"] = "profiles/pmc_traffic.json"
     if rank == 0:
         out = {
+            "lib_sha256": lib_hash,
             "metric": (f"env-steps/sec (end-to-end at the reference update cadence), {args.scenario} N={r.n}, "
                        f"batch {args.batch_size}"),
             "value": round(value, 3),

@@ -263,12 +263,21 @@ class Engine:
     def load_state(self, fname):
         """Restore from a TF1 tensor bundle at prefix `fname` (the reference's
         tf.train.Saver checkpoint, tf_util.py:259-264) or from the .npz
-        save_state writes; when both exist (written by other tools), the newer
-        one."""
+        save_state writes.  save_state removes the other format's files, so
+        both exist only when another tool wrote one of them: then the newer
+        one is read, and equal modification times (a coarse filesystem clock)
+        are refused rather than resolved silently."""
         from .common import tf_checkpoint as tfc
         path = self.checkpoint_path(fname)
-        if tfc.is_bundle(fname) and not (os.path.isfile(path) and
-                                         os.path.getmtime(path) > os.path.getmtime(fname + ".index")):
+        if tfc.is_bundle(fname) and os.path.isfile(path):
+            t_npz, t_tf1 = os.path.getmtime(path), os.path.getmtime(fname + ".index")
+            if t_npz == t_tf1:
+                raise ValueError(f"both {path} and the TF1 bundle {fname}.index exist with the same modification "
+                                 f"time; remove the one not to restore")
+            use_tf1 = t_tf1 > t_npz
+        else:
+            use_tf1 = tfc.is_bundle(fname)
+        if use_tf1:
             self.load_state_dict(tfc.state_from_tf1(tfc.read_bundle(fname), self.n, self.SETS))
             return fname
         with np.load(path, allow_pickle=False) as z:
@@ -355,7 +364,18 @@ class Engine:
         return out
 
     # ------------------------------------------------------------ training
+    @staticmethod
+    def _sized(what, t, want):
+        """the C side reads exactly `want` elements of an injected index / noise
+        tensor: a short one would be an out-of-bounds device read, so refuse it"""
+        if t is not None and t.numel() != want:
+            raise ValueError(f"{what}: {t.numel()} elements, the update reads {want}")
+
     def update(self, agent, idx=None, u_tgt=None, u_act=None):
+        B, n, A = self.batch_size, self.n, _lib.ACT_DIM
+        self._sized("idx", idx, B)
+        self._sized("u_tgt", u_tgt, n * B * A)
+        self._sized("u_act", u_act, B * A)
         args = []
         for t, dt in ((idx, torch.int32), (u_tgt, torch.float32), (u_act, torch.float32)):
             args.append(None if t is None else t.to(self.device, dt).contiguous())
@@ -376,6 +396,10 @@ class Engine:
     def update_all(self, idx=None, u_tgt=None, u_act=None):
         """one throughput-mode round; idx [n, B], u_tgt [n, n, B, 5], u_act [n, B, 5]
         (injected randomness for parity; None: device streams).  mdp_update_all."""
+        B, n, A = self.batch_size, self.n, _lib.ACT_DIM
+        self._sized("idx", idx, n * B)
+        self._sized("u_tgt", u_tgt, n * n * B * A)
+        self._sized("u_act", u_act, n * B * A)
         args = []
         for t, dt in ((idx, torch.int32), (u_tgt, torch.float32), (u_act, torch.float32)):
             args.append(None if t is None else t.to(self.device, dt).contiguous())
@@ -388,6 +412,9 @@ class Engine:
         """MADDPGAgentTrainer.update(agents, t) in one C call (mdp_agent_update):
         None below the gates (maddpg.py:162-165), else the 6 stats.  u: None or
         [n * B * 5 target-actor uniforms | B * 5 actor-loss uniforms] (flat)."""
+        B, n, A = self.batch_size, self.n, _lib.ACT_DIM
+        self._sized("idx", idx, B)
+        self._sized("u", u, (n + 1) * B * A)
         args = []
         for a, dt in ((idx, torch.int32), (u, torch.float32)):
             args.append(None if a is None else a.to(self.device, dt).contiguous().reshape(-1))

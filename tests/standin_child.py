@@ -1,7 +1,7 @@
 """Child process of tests/test_dp_standin_gpu.py (not collected by pytest).
 
 Runs the library's NATIVE data-parallel path (mdp_dp_init + the RCCL calls
-issued from C++) with a world of G = 2 on one GPU: MDP_RCCL_LIB points the
+issued from C++) with a world of G = 2 (MDP_STANDIN_G: any power of two, e.g. 8) on one GPU: MDP_RCCL_LIB points the
 library's dlopen at tests/rccl_standin/libnccl_standin.so, whose
 ncclAllReduce multiplies in place by the communicator size -- the sum over two
 replicas holding this rank's data -- and logs every call.  The RCCL library is
@@ -25,7 +25,7 @@ from maddpg_amd.engine import Engine  # noqa: E402
 from oracle import trainer  # noqa: E402
 from tests.helpers import joint_rows, synthetic_trainer_case  # noqa: E402
 
-G = 2
+G = int(os.environ.get("MDP_STANDIN_G", "2"))   # communicator size (a power of two: x G is exact)
 SETS = ("actor", "critic", "tgt_actor", "tgt_critic", "m_actor", "v_actor", "m_critic", "v_critic")
 
 

@@ -1,0 +1,68 @@
+"""`bench.py --gpus N` is N ranks or no line (CPU tests of the launch contract).
+
+The driver runs the multi-GPU series as `torchrun --nproc-per-node N bench.py
+--gpus N`; a bare `python bench.py --gpus N` (no WORLD_SIZE) must not measure
+and report a one-GPU world under n_gpus = N.  bench.rank_launch_plan decides:
+torchrun's environment present -> it must agree with --gpus; absent with N > 1
+-> start the N rank processes as a child torchrun (fresh processes, before any
+GPU call in this one).  `--launch-check` makes every rank report its
+(rank, world) and exit before touching the GPU, so the real launch runs here.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_plan_single_gpu_runs_in_process():
+    assert bench.rank_launch_plan(1, {}, []) is None
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_plan_without_world_size_launches_n_ranks(n):
+    plan = bench.rank_launch_plan(n, {}, ["--gpus", str(n), "--steps", "7"], port=29555)
+    assert plan[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert f"--nproc-per-node={n}" in plan and "--nnodes=1" in plan
+    assert plan[plan.index("--master-addr") + 1] == "127.0.0.1"
+    assert plan[plan.index("--master-port") + 1] == "29555"
+    assert plan[-4:] == ["--gpus", str(n), "--steps", "7"]
+    assert os.path.basename(plan[-5]) == "bench.py"
+
+
+def test_plan_under_torchrun_runs_in_process():
+    assert bench.rank_launch_plan(8, {"WORLD_SIZE": "8", "RANK": "3"}, []) is None
+
+
+@pytest.mark.parametrize("gpus,ws", [(8, "1"), (8, "4"), (2, "8"), (1, "2")])
+def test_plan_world_size_mismatch_exits_nonzero(gpus, ws):
+    with pytest.raises(SystemExit) as e:
+        bench.rank_launch_plan(gpus, {"WORLD_SIZE": ws}, [])
+    assert e.value.code not in (0, None)
+
+
+def _run(args, **env):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=e,
+                          capture_output=True, text=True, timeout=240)
+
+
+def test_bare_gpus_2_starts_two_ranks():
+    """the real launch path on the CPU: python bench.py --gpus 2 -> torchrun child -> 2 ranks"""
+    r = _run(["--gpus", "2", "--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = sorted((d["rank"], d["world"], d["local_rank"], d["gpus"])
+                 for d in (json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")))
+    assert got == [(0, 2, 0, 2), (1, 2, 1, 2)]
+
+
+def test_world_size_disagreeing_with_gpus_fails():
+    r = _run(["--gpus", "8", "--launch-check"], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    assert r.returncode == 2
+    assert "refusing" in r.stderr and not r.stdout.strip()

@@ -133,7 +133,7 @@ def _run_ranks(world, mode):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_strict_round_ranks_match_full_batch(world):
     res = _run_ranks(world, "strict")
     # equal to the single-process update on the whole batch (reference order)
@@ -163,7 +163,7 @@ def test_strict_round_single_rank_is_update_batch():
             np.testing.assert_array_equal(x.tgt_critic[k], y.tgt_critic[k])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_throughput_round_ranks_match_full_batch(world):
     """throughput mode: ONE all-reduce of every net's gradient per
     round; the replicas equal oracle.trainer.update_round_throughput on the

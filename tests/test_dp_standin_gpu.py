@@ -1,4 +1,4 @@
-"""Native data parallelism at world size 2 on one GPU (the exchange
+"""Native data parallelism at world size 2 and 8 on one GPU (the exchange
 order of maddpg.py:188-194 / train.py:160-161).
 
 The library's native path opens RCCL itself (mdp_dp_init) and issues the
@@ -44,32 +44,34 @@ def _child(mode, **env):
     return out
 
 
-def test_standin_strict_two_allreduces_per_agent_vs_oracle():
-    out = _child("strict", MDP_UNFUSED_APPLY="1")
-    assert out["dp_info"] == {"kind": "rccl", "ranks": 2, "rank": 0, "peers": 1}
+@pytest.mark.parametrize("G", [2, 8])
+def test_standin_strict_two_allreduces_per_agent_vs_oracle(G):
+    out = _child("strict", MDP_UNFUSED_APPLY="1", MDP_STANDIN_G=str(G))
+    assert out["dp_info"] == {"kind": "rccl", "ranks": G, "rank": 0, "peers": G - 1}
     for r in out["rounds"]:
         assert r["allreduces"] == 2 * 3                 # 2N per round
         assert r["spans_match"] and r["in_place"] and r["sum_fp32"]
-        assert r["nranks"] == [2]
-        assert r["dp_vs_single_max_diff"] == 0.0        # (2 g) x 1/2 == g exactly
+        assert r["nranks"] == [G]
+        assert r["dp_vs_single_max_diff"] == 0.0        # (G g) x 1/G == g exactly (G a power of two)
         assert r["stats_equal"]
         assert r["loss_rel_err"] <= 1e-5
         assert r["param_abs_err"] < 2e-4
 
 
-def test_standin_throughput_one_allreduce_per_round_vs_oracle():
-    out = _child("throughput")
+@pytest.mark.parametrize("G", [2, 8])
+def test_standin_throughput_one_allreduce_per_round_vs_oracle(G):
+    out = _child("throughput", MDP_STANDIN_G=str(G))
     assert out["allreduces"] == 1
     assert out["recv_is_grad_base"] and out["covers_every_net"]
-    assert out["nranks"] == [2]
+    assert out["nranks"] == [G]
     assert out["dp_vs_single_max_diff"] == 0.0
     assert out["loss_rel_err"] <= 1e-5
     assert out["param_abs_err"] < 2e-4
 
 
-@pytest.mark.parametrize("graphs", ["0", "1"])
-def test_standin_train_step_matches_single_gpu(graphs):
-    out = _child("graph", MDP_UNFUSED_APPLY="1", MDP_DP_GRAPHS=graphs)
+@pytest.mark.parametrize("graphs,G", [("0", 2), ("1", 2), ("1", 8)])
+def test_standin_train_step_matches_single_gpu(graphs, G):
+    out = _child("graph", MDP_UNFUSED_APPLY="1", MDP_DP_GRAPHS=graphs, MDP_STANDIN_G=str(G))
     assert out["rounds"] == 12
     assert out["dp_vs_single_max_diff"] == 0.0 and out["beta_equal"]
     if graphs == "0":

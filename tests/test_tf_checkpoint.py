@@ -133,7 +133,59 @@ def test_shape_unknown_rank_field():
     """TensorShapeProto field 3 (unknown_rank) present but false is a known-rank
     shape; only unknown_rank = true is refused"""
     dims = tfc._pf_bytes(2, tfc._pf_varint(1, 3)) + tfc._pf_bytes(2, tfc._pf_varint(1, 4))
-    e = tfc._parse_entry(tfc._pf_varint(1, 1) + tfc._pf_bytes(2, dims + tfc._pf_varint(3, 0)))
+    # an explicit field-3 entry with value 0 (tfc._pf_varint omits zero values, so it is
+    # spelled out here): present but false
+    zero = tfc._varint(3 << 3) + tfc._varint(0)
+    assert zero == b"\x18\x00"
+    e = tfc._parse_entry(tfc._pf_varint(1, 1) + tfc._pf_bytes(2, dims + zero))
     assert e["shape"] == [3, 4]
     with pytest.raises(ValueError, match="unknown-rank"):
         tfc._parse_entry(tfc._pf_varint(1, 1) + tfc._pf_bytes(2, tfc._pf_varint(3, 1)))
+
+
+class _FakeEngine:
+    """the attributes Engine.load_state uses, without a GPU"""
+    SETS = ("actor", "critic")
+    n = 1
+
+    def __init__(self):
+        self.loaded = None
+
+    checkpoint_path = staticmethod(lambda f: __import__("maddpg_amd.engine", fromlist=["Engine"]).Engine.checkpoint_path(f))
+
+    def load_state_dict(self, sd):
+        self.loaded = sd
+
+
+def test_load_state_picks_newer_format_and_refuses_a_tie(tmp_path):
+    import os
+
+    from maddpg_amd.engine import Engine
+    sd = _state(1)
+    prefix = str(tmp_path / "ckpt")
+    tfc.write_bundle(prefix, tfc.tf1_from_state(sd))
+    npz = Engine.checkpoint_path(prefix)
+    marked = dict(sd)
+    marked["agent_0/actor/W1"] = sd["agent_0/actor/W1"] + 1.0
+    np.savez(npz, **marked)
+    e = _FakeEngine()
+    os.utime(prefix + ".index", (1000, 1000))
+    os.utime(npz, (2000, 2000))
+    assert Engine.load_state(e, prefix) == npz
+    np.testing.assert_array_equal(e.loaded["agent_0/actor/W1"], marked["agent_0/actor/W1"])
+    os.utime(npz, (500, 500))
+    assert Engine.load_state(e, prefix) == prefix
+    np.testing.assert_array_equal(e.loaded["agent_0/actor/W1"], sd["agent_0/actor/W1"])
+    os.utime(npz, (1000, 1000))
+    with pytest.raises(ValueError, match="same modification time"):
+        Engine.load_state(e, prefix)
+
+
+def test_injected_tensor_sizes_are_checked():
+    import torch
+
+    from maddpg_amd.engine import Engine
+    Engine._sized("idx", None, 1024)
+    Engine._sized("idx", torch.zeros(1024), 1024)
+    with pytest.raises(ValueError, match="idx: 1000 elements, the update reads 1024"):
+        Engine._sized("idx", torch.zeros(1000), 1024)

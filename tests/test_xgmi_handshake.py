@@ -71,19 +71,21 @@ def _run(fail_rank, fail_at, world=2):
     return got
 
 
-def test_all_ranks_enable_with_handles_in_rank_order():
-    got = _run(None, None)
-    for r in range(2):
+@pytest.mark.parametrize("world", [2, 8])
+def test_all_ranks_enable_with_handles_in_rank_order(world):
+    got = _run(None, None, world)
+    for r in range(world):
         ok, has_err, log, handles = got[r]
         assert ok and not has_err
         assert log == ["open", "connect", "probe", "enable"]
-        assert handles == [bytes([0]) * 64, bytes([1]) * 64]
+        assert handles == [bytes([q]) * 64 for q in range(world)]
 
 
-@pytest.mark.parametrize("fail_rank,fail_at", [(1, "open"), (0, "connect"), (1, "probe")])
-def test_any_failure_closes_every_rank(fail_rank, fail_at):
-    got = _run(fail_rank, fail_at)
-    for r in range(2):
+@pytest.mark.parametrize("fail_rank,fail_at,world", [(1, "open", 2), (0, "connect", 2), (1, "probe", 2),
+                                                     (5, "open", 8), (7, "probe", 8)])
+def test_any_failure_closes_every_rank(fail_rank, fail_at, world):
+    got = _run(fail_rank, fail_at, world)
+    for r in range(world):
         ok, has_err, log, _ = got[r]
         assert not ok
         assert log[-1] == "close" and "enable" not in log
@@ -150,9 +152,8 @@ def _select_worker(rank, world, port, stall_rank, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("stall_rank", [0, 1])
-def test_probe_timeout_falls_back_to_rccl_on_every_rank(stall_rank):
-    world = 2
+@pytest.mark.parametrize("stall_rank,world", [(0, 2), (1, 2), (6, 8)])
+def test_probe_timeout_falls_back_to_rccl_on_every_rank(stall_rank, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()

@@ -4,6 +4,8 @@
         --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --bench gpurun_out/prof_bench.json
 
 Writes profiles/<tag>_kernel_stats.csv (the --kernel-trace --stats summary),
+profiles/<tag>_lib.json (the sha256 of the library every bench line of the run
+loaded -- they must agree),
 profiles/<tag>_pmc.csv (per-kernel average FETCH_SIZE / WRITE_SIZE per launch)
 and updates profiles/pmc_traffic.json, which bench.py reads for the
 roofline's `traffic` field.  HBM bytes per launch follow
@@ -60,12 +62,32 @@ def main():
     avg_ns = {short(r["Name"]): float(r["AverageNs"]) for r in rows}
     key = a.config_key
     bench = None
+    lib = None
     if a.bench and os.path.exists(a.bench):
         bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
+        lib = bench.get("lib_sha256")
         if key is None:
             cfg = bench["config"]
             key = f"{cfg['scenario']}_E{cfg['num_envs_per_gpu']}_B{cfg['global_batch'] // bench['n_gpus']}_H64"
         shutil.copy(a.bench, os.path.join(prof, f"{a.tag}_bench.json"))
+    # every bench line of the run (trace, PMC passes, plain bench) must come from ONE
+    # library build: its sha256 goes with the summary, and bench.py uses the committed
+    # durations only for that build
+    seen = {}
+    run_dir = os.path.dirname(os.path.normpath(a.trace))
+    for f in sorted(os.listdir(run_dir)):
+        if f.endswith(".json"):
+            try:
+                line = json.loads(open(os.path.join(run_dir, f)).read().strip().splitlines()[-1])
+            except (ValueError, IndexError):
+                continue
+            if isinstance(line, dict) and line.get("lib_sha256"):
+                seen[f] = line["lib_sha256"]
+    if len(set(seen.values())) > 1:
+        raise SystemExit(f"bench lines of {run_dir} come from different library builds: {seen}")
+    lib = lib or next(iter(seen.values()), None)
+    json.dump({"tag": a.tag, "lib_sha256": lib, "bench_lines": seen, "config_key": key},
+              open(os.path.join(prof, f"{a.tag}_lib.json"), "w"), indent=1, sort_keys=True)
     out = {}
     if a.fetch and a.write:
         fe, wr = counters(a.fetch, "FETCH_SIZE"), counters(a.write, "WRITE_SIZE")
@@ -78,7 +100,7 @@ def main():
                 fp.write(f"{k},{avg_ns.get(k, '')},{fe.get(k, '')},{wr.get(k, '')},{hb:.0f}\n")
         path = os.path.join(prof, "pmc_traffic.json")
         allj = json.load(open(path)) if os.path.exists(path) else {}
-        allj[key] = dict(out, _source=f"{a.tag}_pmc.csv")
+        allj[key] = dict(out, _source=f"{a.tag}_pmc.csv", _lib_sha256=lib)
         json.dump(allj, open(path, "w"), indent=1, sort_keys=True)
     mf = {}
     if a.mfma:
@@ -116,7 +138,7 @@ def main():
                 sq[k] = dict(v, shares=sh)
                 fp.write(f"{k},{avg_ns.get(k, '')}," + ",".join("" if v[n] is None else f"{v[n]:.0f}" for n in names)
                          + "," + ",".join(f"{x:.4f}" for x in sh) + "\n")
-    print(json.dumps({"tag": a.tag, "config_key": key, "avg_ns": avg_ns, "pmc": out, "mfma": mf, "sq": sq}, indent=1))
+    print(json.dumps({"tag": a.tag, "config_key": key, "lib_sha256": lib, "avg_ns": avg_ns, "pmc": out, "mfma": mf, "sq": sq}, indent=1))
 
 
 if __name__ == "__main__":
