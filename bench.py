@@ -330,6 +330,23 @@ def rank_launch_plan(gpus, environ, argv, port=None):
             os.path.join(ROOT, "bench.py")] + list(argv)
 
 
+def run_ranks(plan):
+    """run the torchrun child in its own process group; a SIGTERM / SIGINT to
+    this launcher (a time limit) is passed on to the whole group, so no rank
+    outlives it"""
+    import signal
+    child = subprocess.Popen(plan, cwd=ROOT, start_new_session=True)
+
+    def forward(sig, _frame):
+        try:
+            os.killpg(child.pid, sig)
+        except ProcessLookupError:
+            pass
+    for s in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(s, forward)
+    return child.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -376,7 +393,7 @@ def main():
     # status; a WORLD_SIZE that disagrees with --gpus is an error.
     plan = rank_launch_plan(args.gpus, os.environ, sys.argv[1:])
     if plan is not None:
-        sys.exit(subprocess.run(plan, cwd=ROOT).returncode)
+        sys.exit(run_ranks(plan))
     if args.launch_check:
         print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
                           "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "gpus": args.gpus}))

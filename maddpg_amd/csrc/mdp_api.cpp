@@ -329,10 +329,18 @@ struct mdp_handle {
   bool tp_fits[4] = {true, true, true, true};  // per RaBatch: whole grid co-resident
   std::vector<FusedApplyArgs> tp_host[4];     // the batches' entries, for per-net launches
   RaBatch tp_xchg;                    // data parallel over xGMI: reduce + exchange + step (x 1/G)
+  // general kernels (tp_round_general): agent i's optimizer steps right after
+  // its gradients, as one launch of the [critic_i, actor_i] pair reading the
+  // SHARED slabs (phase 0 single GPU, 1 reduce-only before the all-reduce, 3
+  // xGMI); no Polyak inside (one k_polyak after the round's last step)
+  RaBatch tp_pair[3][MDP_MAX_AGENTS];
+  bool tp_pair_fits[3][MDP_MAX_AGENTS] = {};
+  FusedApplyArgs tp_pair_host[3][MDP_MAX_AGENTS][2];
   // the xGMI batch only when its whole grid is co-resident (every chunk
   // workgroup spins on its peers' matching chunk); otherwise one launch per net
   bool rollout_draw = true;           // step_launches: first-round draw inside k_rollout
   bool draw_ahead = true;             // step_launches: draws one agent ahead (MDP_DRAW_AHEAD=0: per round)
+  bool grad_pair = true;              // throughput mode, general kernels: critic + actor step in one launch (MDP_GRAD_PAIR=0: two)
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
   uint64_t* xbuf = nullptr;
@@ -490,9 +498,10 @@ bool tp_fast(const mdp_handle* h);
 // tp: throughput mode on the general kernels -- this agent's own blocks of
 // partials / stats / TD targets and noise counter upd_ctr + agent (multi = 2
 // marks it; the general kernels take the agent from a.agent, not the grid)
-int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr,
-                   bool tp = false, bool apre = false, const float* u_act = nullptr, int post_prev = -1,
-                   int pf_n = 0) {
+// shared: throughput mode with the strict mode's slab (consumed by this
+// agent's own optimizer launch before the next agent's gradients run)
+CriticArgs critic_args(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, bool tp, int post_prev,
+                       const float* u_act, bool shared) {
   CriticArgs a;
   a.apre = nullptr;
   a.u_act = u_act;
@@ -522,10 +531,22 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
   a.slab_stat = h->stat_c;
   a.y_out = h->y;
   if (tp) {
-    a.slab += (int64_t)agent * h->L.nwg * h->L.slab_c;
+    if (!shared) a.slab += (int64_t)agent * h->L.nwg * h->L.slab_c;
     a.slab_stat += (int64_t)agent * h->L.nwg * 8;
     a.y_out += (int64_t)agent * h->cfg.batch_size;
   }
+  // as many target actors per pass as the LDS budget allows (all of them for S1-S4)
+  const int nact = h->L.topo.ag[agent].local_q ? 1 : h->cfg.n_agents;
+  int G = nact;
+  while (G > 1 && lds_critic_bytes(h->L.topo, G) > MDP_LDS_BUDGET) --G;
+  a.group = G;
+  return a;
+}
+
+int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_tgt, int32_t* pf_out = nullptr,
+                   bool tp = false, bool apre = false, const float* u_act = nullptr, int post_prev = -1,
+                   int pf_n = 0, bool shared = false) {
+  CriticArgs a = critic_args(h, agent, idx, u_tgt, tp, post_prev, u_act, shared);
   ProfScope p(h, MDP_K_CRITIC_GRAD);
   if (!tp && !h->general_grads && grads_r_ok(h->L.topo, agent)) {
     if (pf_out) {  // pf_n indices of the next round's draw (0: all n B of them)
@@ -537,18 +558,13 @@ int do_critic_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_
     HIPCHK(h, mdp_launch_critic_grad_r(a, lds_critic_r_bytes(h->L.topo, agent), h->stream));
     return 0;
   }
-  // as many target actors per pass as the LDS budget allows (all of them for S1-S4)
-  const int nact = h->L.topo.ag[agent].local_q ? 1 : h->cfg.n_agents;
-  int G = nact;
-  while (G > 1 && lds_critic_bytes(h->L.topo, G) > MDP_LDS_BUDGET) --G;
-  if (lds_critic_bytes(h->L.topo, G) > MDP_LDS_BUDGET) return fail(h, "critic step does not fit in LDS");
-  a.group = G;
-  HIPCHK(h, mdp_launch_critic_grad(a, h->L.topo.H, lds_critic_bytes(h->L.topo, G), h->stream));
+  if (lds_critic_bytes(h->L.topo, a.group) > MDP_LDS_BUDGET) return fail(h, "critic step does not fit in LDS");
+  HIPCHK(h, mdp_launch_critic_grad(a, h->L.topo.H, lds_critic_bytes(h->L.topo, a.group), h->stream));
   return 0;
 }
 
-int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, bool tp = false,
-                  bool apre = false, int pre_next = -1, const int32_t* pre_idx = nullptr) {
+ActorArgs actor_args(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, bool tp, bool apre,
+                     int pre_next, const int32_t* pre_idx, bool shared) {
   ActorArgs a;
   a.apre = apre ? h->apre : nullptr;
   a.apre_rows = h->apre_rows;
@@ -574,9 +590,15 @@ int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_a
   a.slab_stride = h->L.slab_a;
   a.slab_stat = h->stat_a;
   if (tp) {
-    a.slab += (int64_t)agent * h->L.nwg * h->L.slab_a;
+    if (!shared) a.slab += (int64_t)agent * h->L.nwg * h->L.slab_a;
     a.slab_stat += (int64_t)agent * h->L.nwg * 8;
   }
+  return a;
+}
+
+int do_actor_grad(mdp_handle* h, int agent, const int32_t* idx, const float* u_act, bool tp = false,
+                  bool apre = false, int pre_next = -1, const int32_t* pre_idx = nullptr, bool shared = false) {
+  ActorArgs a = actor_args(h, agent, idx, u_act, tp, apre, pre_next, pre_idx, shared);
   ProfScope p(h, MDP_K_ACTOR_GRAD);
   if (!tp && !h->general_grads && grads_r_ok(h->L.topo, agent)) {
     int lds = lds_actor_r_bytes(h->L.topo);
@@ -947,13 +969,45 @@ int tp_setup(mdp_handle* h) {
     // phase 1 (reduce only) never spins; the others need the whole batch co-resident
     h->tp_fits[ph] = ph == 1 || rbs[ph]->wg_start[2 * n] <= h->ra_batch_cap;
   }
+  // the per-agent pairs of the general kernels (tp_round_general): shared
+  // slabs, no Polyak, the LAST agent's actor step advancing the noise counter
+  // by n (every gradient launch of the round read upd_ctr + agent before it)
+  const int pair_phase[3] = {0, 1, 3};
+  const size_t pair0 = list.size();
+  for (int pp = 0; pp < 3; ++pp)
+    for (int i = 0; i < n; ++i) {
+      RaBatch& rb = h->tp_pair[pp][i];
+      rb = RaBatch();
+      rb.count = 2;
+      rb.narrow = h->L.nwg <= 64 ? 1 : 0;
+      for (int k = 0; k < 2; ++k) {
+        const int net = 1 - k;  // critic, then actor
+        FusedApplyArgs f = tp_args(h, i, net);
+        f.ap.slab = net ? h->slab_c : h->slab_a;
+        f.ap.polyak = 0;
+        f.ap.bump_ctr = (net == 0 && i == n - 1) ? n : 0;
+        f.phase = pair_phase[pp];
+        if (pp == 2) {
+          if (h->p2p) set_xchg(h, f, i, net);
+          else f.phase = 0;  // unused list
+        }
+        list.push_back(f);
+        h->tp_pair_host[pp][i][k] = f;
+        rb.wg_start[k + 1] = rb.wg_start[k] + mdp_ra_grid(f);
+      }
+      // + the draw workgroup; a reduce-only pass never spins
+      h->tp_pair_fits[pp][i] = pp == 1 || rb.wg_start[2] + 1 <= h->ra_batch_cap;
+    }
   HIPCHK(h, hipMalloc((void**)&h->tp_list, sizeof(FusedApplyArgs) * list.size()));
   HIPCHK(h, hipMemcpy(h->tp_list, list.data(), sizeof(FusedApplyArgs) * list.size(), hipMemcpyHostToDevice));
   for (int ph = 0; ph < 4; ++ph) rbs[ph]->list = h->tp_list + (int64_t)ph * 2 * n;
+  for (int pp = 0; pp < 3; ++pp)
+    for (int i = 0; i < n; ++i) h->tp_pair[pp][i].list = h->tp_list + pair0 + (int64_t)(pp * n + i) * 2;
   return 0;
 }
 
 int dp_allreduce_all(mdp_handle* h);
+int launch_tp_batch(mdp_handle* h, int ph);
 
 // every agent's gradients + every optimizer step; idx [n][B]; optional injected
 // uniforms u_tgt [n][n][B][5] (agent, target actor j, row) and u_act [n][B][5]
@@ -1028,18 +1082,78 @@ int tp_grads_fast(mdp_handle* h, const int32_t* idx, const float* u_tgt, const f
   return 0;
 }
 
-// ... and on the general kernels (H = 128, wide critics): 2n gradient launches
-int tp_grads_general(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
+// agent i's optimizer pair (critic_i, actor_i) in one launch when its grid is
+// co-resident, else one launch per net; `piece`: agent i's B indices of the
+// next round drawn on the side (halves in the per-net launches)
+int launch_tp_pair(mdp_handle* h, int pp, int i, int32_t* piece) {
+  const int B = h->cfg.batch_size;
+  const int kind = pp == 1 ? MDP_K_REDUCE : MDP_K_REDUCE_APPLY;
+  if (h->tp_pair_fits[pp][i]) {
+    RaBatch rb = h->tp_pair[pp][i];
+    if (piece) {
+      rb.pf_out = piece;
+      rb.pf_count = B;
+      rb.pf_ctl = h->ctl;
+    }
+    ProfScope p(h, kind);
+    HIPCHK(h, mdp_launch_reduce_apply_batch(rb, h->stream));
+    return 0;
+  }
+  for (int k = 0; k < 2; ++k) {
+    FusedApplyArgs f = h->tp_pair_host[pp][i][k];
+    if (piece) {
+      f.pf_out = piece + (k ? (B + 1) / 2 : 0);
+      f.pf_count = k ? B - (B + 1) / 2 : (B + 1) / 2;
+      f.pf_ctl = h->ctl;
+    }
+    ProfScope p(h, kind);
+    HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
+  }
+  return 0;
+}
+
+// Throughput mode on the general kernels (H = 128, wide critics): agent by
+// agent, the critic and actor gradients from the round-start parameters, then
+// that agent's two optimizer steps (one launch) -- the partial-gradient slabs
+// are consumed before the next agent's gradients overwrite them, so they stay
+// the strict mode's size (L2 / MALL resident) instead of n per-agent blocks.
+// No agent's gradient reads another agent's actor or critic (the critic input
+// is the replay's actions), only the target actors, so the targets' Polyak is
+// the one thing held back: one k_polyak over every target net after the last
+// step.  The same arithmetic as one batch of every net (update_round_throughput).
+// With RCCL: reduce-only pairs, ONE all-reduce of the whole gradient region,
+// then the step pass (with Polyak) as before.  draw_out: the next round's n B
+// indices, agent i's B in agent i's pair launch (MT19937 stream order).
+int tp_round_general(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* draw_out) {
   const int n = h->cfg.n_agents;
   const int64_t B = h->cfg.batch_size;
+  const int pp = h->comm ? 1 : h->p2p ? 2 : 0;
   int rc;
-  // the next round's draws, which the fast critic kernel makes on the side
-  if (pf_out && (rc = launch_make_index(h, (int)(n * B), pf_out))) return rc;
-  for (int i = 0; i < n; ++i)
-    if ((rc = do_critic_grad(h, i, idx + i * B, u_tgt ? u_tgt + i * n * B * MDP_ACT_DIM : nullptr, nullptr, true)))
-      return rc;
-  for (int i = 0; i < n; ++i)
-    if ((rc = do_actor_grad(h, i, idx + i * B, u_act ? u_act + i * B * MDP_ACT_DIM : nullptr, true))) return rc;
+  for (int i = 0; i < n; ++i) {
+    const int32_t* ix = idx + i * B;
+    const float* ut = u_tgt ? u_tgt + i * n * B * MDP_ACT_DIM : nullptr;
+    const float* ua = u_act ? u_act + i * B * MDP_ACT_DIM : nullptr;
+    if (h->grad_pair) {  // both gradient steps of agent i in one launch
+      GradPairArgs g;
+      g.c = critic_args(h, i, ix, ut, true, -1, nullptr, true);
+      g.x = actor_args(h, i, ix, ua, true, false, -1, nullptr, true);
+      const int lds = std::max(lds_critic_bytes(h->L.topo, g.c.group), lds_actor_bytes(h->L.topo));
+      if (lds > MDP_LDS_BUDGET) return fail(h, "gradient pair does not fit in LDS");
+      ProfScope p(h, MDP_K_CRITIC_GRAD);
+      HIPCHK(h, mdp_launch_grad_pair(g, h->L.topo.H, lds, h->stream));
+    } else {
+      if ((rc = do_critic_grad(h, i, ix, ut, nullptr, true, false, nullptr, -1, 0, true))) return rc;
+      if ((rc = do_actor_grad(h, i, ix, ua, true, false, -1, nullptr, true))) return rc;
+    }
+    if ((rc = launch_tp_pair(h, pp, i, draw_out ? draw_out + i * B : nullptr))) return rc;
+  }
+  if (h->comm) {  // data parallel over RCCL: ONE all-reduce of every net's gradient per round
+    if ((rc = dp_allreduce_all(h))) return rc;
+    ProfScope p(h, MDP_K_APPLY, h->tp_fits[2]);
+    return launch_tp_batch(h, 2);
+  }
+  const ApplyArgs a = apply_args(h, 0, 0, 1.0f);
+  HIPCHK(h, mdp_launch_polyak(h->target, h->theta, h->L.PT, a.pa, a.pb, h->ctl, h->stream));
   return 0;
 }
 
@@ -1056,9 +1170,12 @@ int launch_tp_batch(mdp_handle* h, int ph) {
   return 0;
 }
 
-int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out) {
-  const int rc = tp_fast(h) ? tp_grads_fast(h, idx, u_tgt, u_act, pf_out)
-                            : tp_grads_general(h, idx, u_tgt, u_act, pf_out);
+// pf_out: the next round's draw in the fast critic launch; draw_out: ... in the
+// general path's optimizer launches
+int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out,
+                int32_t* draw_out = nullptr) {
+  if (!tp_fast(h)) return tp_round_general(h, idx, u_tgt, u_act, draw_out);
+  const int rc = tp_grads_fast(h, idx, u_tgt, u_act, pf_out);
   if (rc) return rc;
   if (h->p2p) {  // data parallel over xGMI: reduce + exchange + step of every net, one launch
     ProfScope p(h, MDP_K_REDUCE_APPLY, h->tp_fits[3]);
@@ -1136,6 +1253,8 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
     h->rollout_draw = !(rd && rd[0] == '0');
     const char* da = getenv("MDP_DRAW_AHEAD");
     h->draw_ahead = !(da && da[0] == '0');
+    const char* gp = getenv("MDP_GRAD_PAIR");
+    h->grad_pair = !(gp && gp[0] == '0');
     const char* ap = getenv("MDP_ACTOR_PRE");
     h->actor_pre = !(ap && ap[0] == '0');
     const char* cp = getenv("MDP_CRITIC_PRE");
@@ -1528,7 +1647,7 @@ static int round_updates(mdp_handle* h, const int32_t* idx, int32_t* pf_out = nu
                          int ahead = 0) {
   const int n = h->cfg.n_agents, B = h->cfg.batch_size;
   if (carry_out) *carry_out = false;
-  if (h->update_mode == 1) return do_round_tp(h, idx, nullptr, nullptr, pf_out);
+  if (h->update_mode == 1) return do_round_tp(h, idx, nullptr, nullptr, pf_out, draw_out);
   const int nb = n * B, piece = (nb + 2 * n - 1) / (2 * n);
   // the next round's draw (pf_out) in per-agent pieces, agent i's B indices in
   // agent i's critic launch -- the stream order of one n B draw (every launch
@@ -1983,7 +2102,8 @@ static int step_launches(mdp_handle* h, int rounds) {
   const int nb = h->cfg.n_agents * h->cfg.batch_size;
   int32_t* slot[2] = {h->index, h->index + nb};
   const bool pf = prefetch_ok(h);
-  const bool ra_draw = !pf && h->update_mode == 0 && draw_in_ra_ok(h);
+  // (throughput mode on the general kernels: in its optimizer pair launches, RCCL included)
+  const bool ra_draw = !pf && (h->update_mode == 0 ? draw_in_ra_ok(h) : !tp_fast(h));
   bool fast_all = !h->general_grads;
   for (int i = 0; i < h->cfg.n_agents && fast_all; ++i) fast_all = grads_r_ok(h->L.topo, i);
   // one agent ahead (round_updates): the step's first draw is agent 0's B only

@@ -171,6 +171,29 @@ hipError_t mdp_launch_xchg_probe(const XchgDesc* xd, uint32_t ep, int nchunk, ui
   return hipGetLastError();
 }
 
+// diagnostic build only: per-workgroup phase stamps of the last critic-step
+// (sel 0) and actor-step (sel 1) optimizer launch (tools/ra_budget.py)
+#ifdef MDP_STAMPS
+__device__ unsigned long long g_ra_ph[2][1024][8];
+#define MDP_RA_PH(k)                                                                                     \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && b < 1024) g_ra_ph[a.stats_mode == 1 ? 0 : 1][b][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+extern "C" int mdp_debug_ra_phases(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ra_ph), sizeof(g_ra_ph)) == hipSuccess ? 0 : -1;
+}
+extern "C" int mdp_debug_ra_phases_reset() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_ra_ph)) != hipSuccess) return -1;
+  return hipMemset(p, 0, sizeof(unsigned long long) * 2 * 1024 * 8) == hipSuccess && hipDeviceSynchronize() == hipSuccess
+             ? 0 : -1;
+}
+#else
+#define MDP_RA_PH(k) \
+  do {               \
+  } while (0)
+#endif
+
 // ((r0 + r1) + (r2 + r3)) + ... over rows [LO, LO + N) of the group sums
 // (compile-time indices: a private array here stayed in scratch)
 template <int LO, int N>
@@ -194,6 +217,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
   __shared__ float step_l[4];      // beta1^t, beta2^t, the tensor norm, fault
   const int tid = threadIdx.x, lane = tid & 63;
   MDP_STAMP(30);
+  MDP_RA_PH(0);
   if (f.phase == 1 && b >= f.rblk[6]) return;  // reduce-only pass: chunk workgroups only
   if (b < f.rblk[6]) {
     int t = 0;
@@ -278,6 +302,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     }
     __syncthreads();
     MDP_STAMP(31);
+    MDP_RA_PH(1);
     if (grp == 0 && f.phase != 1 && a.stats_mode) {
       // arrival: this workgroup has its step's beta powers and epochs in
       // registers (loaded first, vmcnt drained), so the stats workgroup may
@@ -300,6 +325,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       }
       ss = wave_sum_d(ss);
       MDP_STAMP(35);
+      MDP_RA_PH(2);
       // the norm handshake's publish goes out first (its round trip is the
       // launch's longest wait), the reduced-gradient stores behind it
       uint64_t* part = f.sync_part + (int64_t)t * MDP_RA_MAXCH * 2;
@@ -321,6 +347,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
         }
       }
       MDP_STAMP(36);
+      MDP_RA_PH(3);
       double tot = ss;
       if (f.phase != 1) {  // phase 1 (data parallel) stops here: the all-reduce follows
       if (nch > 1) {
@@ -352,6 +379,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       if (f.phase == 3)
         faulted = faulted || __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
       MDP_STAMP(37);
+      MDP_RA_PH(4);
       // the chunk's gradient, this step's powers, the norm and the fault state
       // to the Adam waves
       gl[col] = g;
@@ -457,6 +485,10 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
     }
   }
   MDP_STAMP(33);
+#ifdef MDP_STAMPS
+  __syncthreads();  // (every wave's Adam / Polyak / stats stores issued)
+#endif
+  MDP_RA_PH(5);
   if (f.phase == 1) return;  // uniform: the whole grid of a reduce-only pass
   if (a.stats_mode) {
     // the stats workgroup advances the optimizer step once every chunk
@@ -472,6 +504,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
           break;
         }
       }
+      MDP_RA_PH(6);
       __hip_atomic_store(f.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
         const float p1 = a.beta[0], p2 = a.beta[1];
@@ -483,6 +516,7 @@ __device__ __forceinline__ void reduce_apply_body(const FusedApplyArgs& f, const
       if (a.bump_ctr) a.ctl->upd_ctr += (uint32_t)a.bump_ctr;
       if (f.phase == 3) f.xstep[0] += 1u;
       f.sync_ctr[7 * 32] += 1u;
+      MDP_RA_PH(7);
     }
     return;
   }
@@ -548,6 +582,10 @@ __global__ __launch_bounds__(NT) void k_reduce_apply(FusedApplyArgs f) {
 // workgroups handshake only among themselves; the nets are independent)
 template <int NT>
 __global__ __launch_bounds__(NT) void k_reduce_apply_batch(RaBatch rb) {
+  if (rb.pf_count > 0 && blockIdx.x == gridDim.x - 1) {  // a piece of the next round's index draw
+    make_index_block<NT>(rb.pf_ctl, rb.pf_count, rb.pf_out);
+    return;
+  }
   int q = 0;
   while (q + 1 < rb.count && (int)blockIdx.x >= rb.wg_start[q + 1]) ++q;
   const int b = blockIdx.x - rb.wg_start[q];
@@ -608,10 +646,11 @@ hipError_t mdp_ra_batch_occupancy(int* per_cu) {
 }
 
 hipError_t mdp_launch_reduce_apply_batch(const RaBatch& b, hipStream_t s) {
-  if (MDP_RA_NARROW && b.narrow)  // (no draw piece in a batch)
-    mdp_launch(k_reduce_apply_batch<256>, dim3(b.wg_start[b.count]), dim3(256), 0, s, b);
+  const dim3 grid(b.wg_start[b.count] + (b.pf_count > 0 ? 1 : 0));  // + the draw piece, last
+  if (MDP_RA_NARROW && b.narrow)
+    mdp_launch(k_reduce_apply_batch<256>, grid, dim3(256), 0, s, b);
   else
-    mdp_launch(k_reduce_apply_batch<1024>, dim3(b.wg_start[b.count]), dim3(1024), 0, s, b);
+    mdp_launch(k_reduce_apply_batch<1024>, grid, dim3(1024), 0, s, b);
   return hipGetLastError();
 }
 

@@ -525,13 +525,14 @@ __device__ __forceinline__ void wgrad_tile(const float* X, int ldx, int K, const
 
 static_assert(MDP_GEN_THREADS / 64 >= MDP_MAX_UNITS / 16, "one single-net layer tile per wave (pf_load / *_pf)");
 
+// blk: this workgroup's row tile (blockIdx.x, or its index inside the
+// critic half of a gradient-pair launch)
 template <int H>
-__global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
+__device__ __forceinline__ void critic_body(const CriticArgs& a, const Topo& T, const int blk) {
   // (no MDP_KARG_TOUCH here: at H = 128 it turned the kernel's 47 spilled
   // SGPRs into 91 spilled VGPRs)
   constexpr int NT = H / 16;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Topo& T = a.topo;
   const ADesc& ag = T.ag[a.agent];
   const int G = a.group;
   const int ldr = lds_ld(T.row_stride), ldc = lds_ld(T.cin_max), ldh = H + 1;
@@ -548,7 +549,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
                                                                     // work-queue counter (fwd_phase_l12)
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = blockDim.x >> 6;
-  const int r0 = blockIdx.x * MDP_R;
+  const int r0 = blk * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const bool lq = ag.local_q != 0;
   // throughput mode (multi > 1: one launch per agent, every agent from the
@@ -783,7 +784,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
     s_r = sum16(s_r);
     s_q = sum16(s_q);
     if (lane == 0) {
-      double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+      double* st = a.slab_stat + (int64_t)blk * 8;
       st[0] = s_l;
       st[1] = s_y;
       st[2] = s_r;
@@ -794,7 +795,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
   MDP_STAMP(3);
 
   // backward through the critic (tf.gradients of q_loss w.r.t. q_func vars)
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - nd.off;
+  float* slab = a.slab + (int64_t)blk * a.slab_stride - nd.off;
   float* d2 = hA;
   float* d1 = hB;
   if (tid < H) {
@@ -824,12 +825,15 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
 }
 
 template <int H>
-__global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
-  MDP_KARG_TOUCH("s"(a.agent), "s"(a.slab_stride), "s"(a.cpre_agent), "s"(a.topo.n));
-  MDP_KARG_TOUCH(MDP_KARG_ADESC(a.topo.ag[a.agent]));
+__global__ __launch_bounds__(MDP_GEN_THREADS) void k_critic_grad(CriticArgs a) {
+  critic_body<H>(a, a.topo, blockIdx.x);
+}
+
+// AA: ActorArgs, or the Topo-less ActorArgsHead of a gradient-pair launch
+template <int H, class AA>
+__device__ __forceinline__ void actor_body(const AA& a, const Topo& T, const int blk) {
   constexpr int NT = H / 16;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Topo& T = a.topo;
   const ADesc& ag = T.ag[a.agent];
   const int ldr = lds_ld(T.row_stride), ldc = lds_ld(T.cin_max), ldh = H + 1;
   const int S = MDP_R * ldh;
@@ -850,7 +854,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   float* w1ai = cv.take(MDP_ACT_DIM * H);  // the critic's layer-1 rows of the a_i input (for da)
 
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = blockDim.x >> 6;
-  const int r0 = blockIdx.x * MDP_R;
+  const int r0 = blk * MDP_R;
   const int nvalid = min(MDP_R, a.B - r0);
   const bool lq = ag.local_q != 0;
   // throughput mode (multi > 1: one launch per agent, every agent from the
@@ -1035,7 +1039,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
     s_q = sum16(s_q);
     s_p = sum16(s_p);
     if (lane == 0) {
-      double* st = a.slab_stat + (int64_t)blockIdx.x * 8;
+      double* st = a.slab_stat + (int64_t)blk * 8;
       st[0] = s_q;
       st[1] = s_p;
     }
@@ -1043,7 +1047,7 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   __syncthreads();
   MDP_STAMP(57);
   // actor backward: dW3a, db3a, d2a = (dl @ W3a^T) masked by h2a > 0
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride - na.off;
+  float* slab = a.slab + (int64_t)blk * a.slab_stride - na.off;
   const float* W3a = P + na.t[4].off;
   for (int e = tid; e < H * MDP_ACT_DIM; e += blockDim.x) {
     const int h = e / MDP_ACT_DIM, k = e - h * MDP_ACT_DIM;
@@ -1077,6 +1081,23 @@ __global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
   MDP_STAMP(60);
 }
 
+template <int H>
+__global__ __launch_bounds__(MDP_GEN_THREADS) void k_actor_grad(ActorArgs a) {
+  MDP_KARG_TOUCH("s"(a.agent), "s"(a.slab_stride), "s"(a.cpre_agent), "s"(a.topo.n));
+  MDP_KARG_TOUCH(MDP_KARG_ADESC(a.topo.ag[a.agent]));
+  actor_body<H>(a, a.topo, blockIdx.x);
+}
+
+// throughput mode: agent i's critic step (workgroups [0, B/16)) and actor step
+// (the rest) in one launch -- no kernel boundary between them, and the actor
+// step's workgroups start on the CUs the critic step's finished ones free
+template <int H>
+__global__ __launch_bounds__(MDP_GEN_THREADS) void k_grad_pair(GradPairArgs p) {
+  const int nc = (p.c.B + MDP_R - 1) / MDP_R;
+  if ((int)blockIdx.x < nc) critic_body<H>(p.c, p.c.topo, blockIdx.x);
+  else actor_body<H>(p.x, p.c.topo, (int)blockIdx.x - nc);
+}
+
 // ---------------------------------------------------------------- launchers
 namespace {
 template <int H>
@@ -1104,6 +1125,28 @@ hipError_t launch_actor(const ActorArgs& a, int lds, hipStream_t s) {
   return hipGetLastError();
 }
 }  // namespace
+
+template <int H>
+hipError_t launch_pair(const GradPairArgs& a, int lds, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_grad_pair<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              MDP_LDS_BUDGET);
+    (void)hipGetLastError();
+    attr = true;
+  }
+  mdp_launch(k_grad_pair<H>, dim3(2 * ((a.c.B + MDP_R - 1) / MDP_R)), dim3(MDP_GEN_THREADS), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t mdp_launch_grad_pair(const GradPairArgs& a, int H, int lds_bytes, hipStream_t s) {
+  switch (H) {
+    case 64: return launch_pair<64>(a, lds_bytes, s);
+    case 128: return launch_pair<128>(a, lds_bytes, s);
+    case 256: return launch_pair<256>(a, lds_bytes, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s) {
   switch (H) {

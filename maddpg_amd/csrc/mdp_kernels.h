@@ -67,7 +67,8 @@ struct CriticArgs {
 // workgroups -> k_actor_grad_r): h1 [64] | h2 [64] | logits [8] | sample [8]
 #define MDP_APRE_W 144
 
-struct ActorArgs {
+// (the fields without the Topo: the gradient-pair launch passes ONE Topo for both steps)
+struct ActorArgsHead {
   int agent, B;
   const float* theta;
   const float* replay;
@@ -91,7 +92,17 @@ struct ActorArgs {
   int cpre_agent;
   const int32_t* cpre_idx;
   const float* target;        // target nets (the critic_pre role's target actors / critic)
+};
+struct ActorArgs : ActorArgsHead {
   Topo topo;
+};
+
+// throughput mode on the general kernels: agent i's critic step and actor step
+// (independent there: both read the round-start parameters) as ONE launch --
+// workgroups [0, B/16) the critic step, [B/16, 2 B/16) the actor step
+struct GradPairArgs {
+  CriticArgs c;
+  ActorArgsHead x;
 };
 
 struct ReduceArgs {
@@ -327,6 +338,7 @@ inline void mdp_launch(F kernel, const dim3& grid, const dim3& block, uint32_t l
 
 hipError_t mdp_launch_critic_grad(const CriticArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad(const ActorArgs& a, int H, int lds_bytes, hipStream_t s);
+hipError_t mdp_launch_grad_pair(const GradPairArgs& a, int H, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_critic_grad_r(const CriticArgs& a, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_actor_grad_r(const ActorArgs& a, int lds_bytes, hipStream_t s);
 hipError_t mdp_launch_rollout(const RolloutArgs& a, int H, int lds_bytes, hipStream_t s);
@@ -338,10 +350,15 @@ hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s);
 // lives in device memory (written once), wg_start[q] = first workgroup of net q
 #define MDP_RA_BATCH_MAX (2 * MDP_MAX_AGENTS)
 struct RaBatch {
-  const FusedApplyArgs* list;
-  int count;
-  int narrow;           // fan-in <= 64 partials: 256-thread workgroups (mdp_ra_narrow)
-  int wg_start[MDP_RA_BATCH_MAX + 1];
+  const FusedApplyArgs* list = nullptr;
+  int count = 0;
+  int narrow = 0;       // fan-in <= 64 partials: 256-thread workgroups (mdp_ra_narrow)
+  int wg_start[MDP_RA_BATCH_MAX + 1] = {};
+  // pf_count > 0: one extra (last) workgroup draws pf_count indices of the next
+  // round into pf_out, continuing the MT19937 stream in pf_ctl (as FusedApplyArgs)
+  int pf_count = 0;
+  int32_t* pf_out = nullptr;
+  Ctl* pf_ctl = nullptr;
 };
 int mdp_ra_grid(const FusedApplyArgs& f);
 hipError_t mdp_ra_occupancy(int* per_cu);   // co-resident k_reduce_apply workgroups per CU
@@ -375,6 +392,10 @@ hipError_t mdp_ra_batch_occupancy(int* per_cu);
 hipError_t mdp_launch_xchg_probe(const XchgDesc* xd, uint32_t ep, int nchunk, uint32_t* bad, uint32_t* fault,
                                  hipStream_t s);
 hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t s);
+// target <- pa target + pb theta over n floats (make_update_exp, maddpg.py:20-26),
+// skipped once Ctl::fault is set; n a multiple of 4
+hipError_t mdp_launch_polyak(float* target, const float* theta, int64_t n, float pa, float pb, const Ctl* ctl,
+                             hipStream_t s);
 hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
                              hipStream_t s);
 hipError_t mdp_launch_put_rows(float* replay, int stride, int64_t cap, int64_t next, const float* src, int64_t rows,

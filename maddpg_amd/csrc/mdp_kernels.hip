@@ -1127,6 +1127,28 @@ hipError_t mdp_launch_make_index(Ctl* ctl, int count, int32_t* out, hipStream_t 
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
+// Polyak of every target net in one pass (throughput mode: after the round's
+// last optimizer step, so no gradient of the round reads a stepped target)
+__global__ __launch_bounds__(256) void k_polyak(float* __restrict__ target, const float* __restrict__ theta,
+                                                int64_t n4, float pa, float pb, const Ctl* ctl) {
+  if (__hip_atomic_load(&ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 tg = reinterpret_cast<const f32x4*>(target)[i];
+    const f32x4 th = reinterpret_cast<const f32x4*>(theta)[i];
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pa * tg[j] + pb * th[j];  // the fused kernels' expression
+    reinterpret_cast<f32x4*>(target)[i] = o;
+  }
+}
+hipError_t mdp_launch_polyak(float* target, const float* theta, int64_t n, float pa, float pb, const Ctl* ctl,
+                             hipStream_t s) {
+  const int64_t n4 = n / 4;
+  const int grid = (int)std::min<int64_t>(1024, (n4 + 255) / 256);
+  mdp_launch(k_polyak, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, target, theta, n4, pa, pb, ctl);
+  MDP_CHECK_LAUNCH();
+  return hipSuccess;
+}
 hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
                              hipStream_t s) {
   const int v4 = stride >> 2;

@@ -23,7 +23,7 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 # kernels allowed to spill (mangled-name prefixes)
-ALLOWED = ("_Z13k_critic_gradILi",)
+ALLOWED = ("_Z13k_critic_gradILi", "_Z11k_grad_pairILi")  # the general critic step and the pair launch holding it
 
 
 def kernel_scratch(lib):

@@ -21,6 +21,11 @@ run() {  # name nproc env-assignment [bench args...]
 run xgmi2 2 MDP_DP_XGMI=1
 run xgmi4 4 MDP_DP_XGMI=1 --no-throughput-figure
 run torchdist2 2 MDP_NATIVE_DP=0
+# 8 ranks (7 peers per exchange, MDP_XCH_MAXW filled) launched by bench.py itself
+# (--gpus 8 without torchrun's environment), small E per rank
+env MDP_DP_XGMI=1 timeout -k 10 300 python3 bench.py --gpus 8 --num-envs 512 --steps 5 --warmup 2 \
+    --no-throughput-figure > $O/xgmi8.json 2> $O/xgmi8.err
+echo "xgmi8: $(tail -c 400 $O/xgmi8.json)"
 # configs[4]'s topology (general H=128 kernels), 2 ranks over xGMI
 run tag6_xgmi2 2 MDP_DP_XGMI=1 --scenario simple_tag --num-agents 6 --scenario-adversaries 4 \
     --num-adversaries 4 --num-units 128 --batch-size 4096 --num-envs 4096 --steps 5 --no-throughput-figure
