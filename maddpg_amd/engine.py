@@ -123,7 +123,13 @@ class Engine:
 
     @staticmethod
     def _ptr(t):
-        return ctypes.c_void_p(0 if t is None else t.data_ptr())
+        """device pointer of a tensor for the C ABI (null for None).  A host tensor is
+        refused: the kernels would dereference its address on the device."""
+        if t is None:
+            return ctypes.c_void_p(0)
+        if not t.is_cuda:
+            raise ValueError("the C ABI takes device tensors; got a host tensor")
+        return ctypes.c_void_p(t.data_ptr())
 
     def region(self, name, dtype=torch.float32):
         off, nb = ctypes.c_int64(), ctypes.c_int64()
@@ -554,10 +560,22 @@ class Engine:
         self._c("mdp_set_graphs", 1 if on else 0)
 
     def critic_grad(self, agent, idx, u_tgt=None):
+        B, n, A = self.batch_size, self.n, _lib.ACT_DIM
+        self._sized("idx", idx, B)
+        self._sized("u_tgt", u_tgt, n * B * A)
+        idx = idx.to(self.device, torch.int32).contiguous()
+        u_tgt = None if u_tgt is None else u_tgt.to(self.device, torch.float32).contiguous()
         self._c("mdp_critic_grad", agent, self._ptr(idx), self._ptr(u_tgt))
+        self._keep = (idx, u_tgt)
 
     def actor_grad(self, agent, idx, u_act=None):
+        B, A = self.batch_size, _lib.ACT_DIM
+        self._sized("idx", idx, B)
+        self._sized("u_act", u_act, B * A)
+        idx = idx.to(self.device, torch.int32).contiguous()
+        u_act = None if u_act is None else u_act.to(self.device, torch.float32).contiguous()
         self._c("mdp_actor_grad", agent, self._ptr(idx), self._ptr(u_act))
+        self._keep = (idx, u_act)
 
     def reduce_grad(self, agent, net):
         self._c("mdp_reduce_grad", agent, net)

@@ -58,9 +58,12 @@ def test_standin_strict_two_allreduces_per_agent_vs_oracle(G):
         assert r["param_abs_err"] < 2e-4
 
 
-@pytest.mark.parametrize("G", [2, 8])
-def test_standin_throughput_one_allreduce_per_round_vs_oracle(G):
-    out = _child("throughput", MDP_STANDIN_G=str(G))
+@pytest.mark.parametrize("G,general", [(2, "0"), (8, "0"), (2, "1")])
+def test_standin_throughput_one_allreduce_per_round_vs_oracle(G, general):
+    # general = "1": the general kernels' round (per-agent gradient pairs and
+    # reduce-only optimizer pairs, then the one all-reduce and the step pass)
+    # against the single-GPU general round (optimizer pairs + k_polyak)
+    out = _child("throughput", MDP_STANDIN_G=str(G), MDP_GENERAL_GRADS=general)
     assert out["allreduces"] == 1
     assert out["recv_is_grad_base"] and out["covers_every_net"]
     assert out["nranks"] == [G]

@@ -189,3 +189,12 @@ def test_injected_tensor_sizes_are_checked():
     Engine._sized("idx", torch.zeros(1024), 1024)
     with pytest.raises(ValueError, match="idx: 1000 elements, the update reads 1024"):
         Engine._sized("idx", torch.zeros(1000), 1024)
+
+
+def test_host_tensors_are_refused_at_the_abi():
+    import torch
+
+    from maddpg_amd.engine import Engine
+    assert Engine._ptr(None).value is None
+    with pytest.raises(ValueError, match="device tensors"):
+        Engine._ptr(torch.zeros(4, dtype=torch.int32))
