@@ -341,6 +341,10 @@ struct mdp_handle {
   bool rollout_draw = true;           // step_launches: first-round draw inside k_rollout
   bool draw_ahead = true;             // step_launches: draws one agent ahead (MDP_DRAW_AHEAD=0: per round)
   bool grad_pair = true;              // throughput mode, general kernels: critic + actor step in one launch (MDP_GRAD_PAIR=0: two)
+#ifdef MDP_EXP_TPRE
+  Topo* tp_exp_topo = nullptr;        // timing-only experiment: device copy of the topology
+  float* tp_exp_out = nullptr;        // ... and its a~ scratch [B][32]
+#endif
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
   uint64_t* xbuf = nullptr;
@@ -698,6 +702,9 @@ FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net, bool tp = false
   f.pf_count = 0;
   f.pf_out = nullptr;
   f.pf_ctl = h->ctl;
+#ifdef MDP_EXP_TPRE
+  f.tp_count = 0;
+#endif
   return f;
 }
 
@@ -733,6 +740,21 @@ int do_reduce_apply(mdp_handle* h, int agent, int net, int32_t* pf_out = nullptr
     f.pf_out = pf_out;
     f.pf_count = pf_count;
   }
+#ifdef MDP_EXP_TPRE  // timing only: the next agent's target-actor forwards on the idle CUs
+  if (h->tp_exp_topo && h->L.topo.H == 128 && h->cfg.n_agents > 1 && h->update_mode == 0) {
+    const int half = (h->L.nwg + 1) / 2;
+    f.tp_count = net ? half : (int)h->L.nwg - half;
+    f.tp_agent = (agent + 1) % h->cfg.n_agents;
+    f.tp_skip = agent;
+    f.tp_B = h->cfg.batch_size;
+    f.tp_topo = h->tp_exp_topo;
+    f.tp_replay = h->replay;
+    f.tp_target = h->target;
+    f.tp_idx = h->index;
+    f.tp_seed = h->cfg.seed;
+    f.tp_out = h->tp_exp_out;
+  }
+#endif
   if (h->p2p) set_xchg(h, f, agent, net);
   ProfScope p(h, MDP_K_REDUCE_APPLY);
   HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
@@ -1347,6 +1369,11 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
   std::memset(&c, 0, sizeof(c));
   py_seed_state(0, c.mt, &c.mt_pos);
   HIPCHK(h, hipMemcpyAsync(h->ctl, &c, sizeof(c), hipMemcpyHostToDevice, h->stream));
+#ifdef MDP_EXP_TPRE
+  HIPCHK(h, hipMalloc((void**)&h->tp_exp_topo, sizeof(Topo)));
+  HIPCHK(h, hipMemcpyAsync(h->tp_exp_topo, &h->L.topo, sizeof(Topo), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMalloc((void**)&h->tp_exp_out, sizeof(float) * 32 * (size_t)cfg->batch_size));
+#endif
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->err.clear();
   return 0;
