@@ -128,9 +128,10 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
   if (c->n_agents < 1 || c->n_agents > MDP_MAX_AGENTS) { err = "n_agents out of range"; return false; }
   if (c->act_dim != MDP_ACT_DIM) { err = "act_dim must be 5 (MPE Discrete(5))"; return false; }
   if (c->num_units < 1 || c->num_units > MDP_MAX_UNITS) { err = "num_units must be in [1, 256]"; return false; }
-  if (c->batch_size < 1) { err = "batch_size must be >= 1"; return false; }
+  // upper bounds keep every row / index count of a launch inside int32
+  if (c->batch_size < 1 || c->batch_size > (1 << 20)) { err = "batch_size must be in [1, 2^20]"; return false; }
   if (c->capacity < 1 || c->capacity > (int64_t(1) << 31) - 1) { err = "capacity out of range"; return false; }
-  if (c->num_envs < 0) { err = "num_envs < 0"; return false; }
+  if (c->num_envs < 0 || c->num_envs > (1 << 24)) { err = "num_envs must be in [0, 2^24]"; return false; }
   // --num-units is any width (train.py:24); the device nets are H wide with H
   // the kernel width that holds it.  The extra hidden units have zero weights
   // and biases: relu(0) = 0 feeds nothing forward, their gradients are exactly
@@ -279,6 +280,7 @@ struct mdp_handle {
   uint32_t act_ctr = 0, reset_ctr = 0;
   bool env_lockstep = true;   // every env copy at the same episode step (log in env order)
   std::string err;
+  bool ready = false;  // mdp_create finished: arena, stream and layout bound
   bool prof_on[MDP_K_COUNT] = {};
   std::vector<hipEvent_t> ev[MDP_K_COUNT];
   size_t ev_used[MDP_K_COUNT] = {};
@@ -376,6 +378,15 @@ int fail(mdp_handle* h, const char* what, hipError_t e = hipSuccess) {
     if (e__ != hipSuccess) return fail(h, #call, e__); \
   } while (0)
 
+// every entry point on a handle refuses a null one and one whose mdp_create
+// failed (no arena or stream bound: nothing may be launched on it); the
+// create error stays in mdp_last_error
+bool unusable(const mdp_handle* h) { return !h || !h->ready; }
+#define MDP_NEED(h)               \
+  do {                            \
+    if (unusable(h)) return -1;   \
+  } while (0)
+
 }  // namespace
 
 MdpLaunchEv& mdp_launch_ev() {
@@ -444,6 +455,7 @@ void flush_prof(mdp_handle* h, int kind) {
 }
 
 bool bad_agent(mdp_handle* h, int agent) {
+  if (unusable(h)) return true;
   if (agent < 0 || agent >= h->cfg.n_agents) {
     fail(h, "agent index out of range");
     return true;
@@ -1376,6 +1388,7 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
 #endif
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->err.clear();
+  h->ready = true;
   return 0;
 }
 
@@ -1400,6 +1413,7 @@ const char* mdp_last_error(const mdp_handle* h) { return h ? h->err.c_str() : "n
 void* mdp_stream(mdp_handle* h) { return h ? (void*)h->stream : nullptr; }
 
 int mdp_synchronize(mdp_handle* h) {
+  MDP_NEED(h);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   uint32_t fault = 0;
   HIPCHK(h, hipMemcpy(&fault, &h->ctl->fault, sizeof(fault), hipMemcpyDeviceToHost));
@@ -1410,14 +1424,14 @@ int mdp_synchronize(mdp_handle* h) {
 }
 
 int mdp_region(const mdp_handle* h, int32_t region, int64_t* offset, int64_t* bytes) {
-  if (!h || region < 0 || region >= MDP_R_COUNT) return -1;
+  if (unusable(h) || region < 0 || region >= MDP_R_COUNT) return -1;
   if (offset) *offset = h->L.off[region];
   if (bytes) *bytes = h->L.bytes[region];
   return 0;
 }
 
 int mdp_tensor(const mdp_handle* h, int32_t agent, int32_t net, int32_t t, mdp_tensor_info* out) {
-  if (!h || agent < 0 || agent >= h->cfg.n_agents || t < 0 || t > 5 || !out) return -1;
+  if (unusable(h) || agent < 0 || agent >= h->cfg.n_agents || t < 0 || t > 5 || !out) return -1;
   const NDesc& d = net ? h->L.topo.ag[agent].critic : h->L.topo.ag[agent].actor;
   out->offset = d.t[t].off;
   logical_shape(h, d, t, &out->rows, &out->cols);
@@ -1427,7 +1441,7 @@ int mdp_tensor(const mdp_handle* h, int32_t agent, int32_t net, int32_t t, mdp_t
 }
 
 int mdp_row_layout(const mdp_handle* h, int32_t agent, int32_t out6[6]) {
-  if (!h || agent < 0 || agent >= h->cfg.n_agents) return -1;
+  if (unusable(h) || agent < 0 || agent >= h->cfg.n_agents) return -1;
   const ADesc& a = h->L.topo.ag[agent];
   out6[0] = a.obs_off;
   out6[1] = a.act_off;
@@ -1493,9 +1507,10 @@ int mdp_set_beta_powers(mdp_handle* h, int32_t agent, int32_t net, const float i
 }
 
 // ----------------------------------------------------------------- replay
-int64_t mdp_buffer_len(mdp_handle* h) { return h ? h->len : -1; }
+int64_t mdp_buffer_len(mdp_handle* h) { return unusable(h) ? -1 : h->len; }
 
 int mdp_buffer_add_rows(mdp_handle* h, const float* rows_dev, int64_t rows) {
+  MDP_NEED(h);
   if (rows < 0) return fail(h, "negative row count");
   if (rows == 0) return 0;
   const int64_t cap = h->cfg.capacity;
@@ -1517,12 +1532,14 @@ int mdp_buffer_put_agent(mdp_handle* h, int32_t agent, const int64_t* pos_dev, c
 }
 
 int mdp_buffer_set_len(mdp_handle* h, int64_t len, int64_t next_idx) {
+  MDP_NEED(h);
   if (len < 0 || len > h->cfg.capacity || next_idx < 0 || next_idx >= h->cfg.capacity)
     return fail(h, "ring state out of range");
   return set_ring(h, len, next_idx);
 }
 
 int mdp_seed_py_random(mdp_handle* h, uint64_t seed) {
+  MDP_NEED(h);
   Ctl c;
   py_seed_state(seed, c.mt, &c.mt_pos);
   HIPCHK(h, hipMemcpyAsync(h->ctl->mt, c.mt, sizeof(c.mt) + sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
@@ -1531,6 +1548,8 @@ int mdp_seed_py_random(mdp_handle* h, uint64_t seed) {
 }
 
 int mdp_set_rng_state(mdp_handle* h, const uint32_t* st) {
+  MDP_NEED(h);
+  if (!st) return fail(h, "null RNG state");
   if (st[624] > 624) return fail(h, "MT position out of range");
   uint32_t buf[625];
   std::memcpy(buf, st, sizeof(buf));
@@ -1540,18 +1559,22 @@ int mdp_set_rng_state(mdp_handle* h, const uint32_t* st) {
 }
 
 int mdp_get_rng_state(mdp_handle* h, uint32_t* st) {
+  MDP_NEED(h);
+  if (!st) return fail(h, "null RNG state");
   HIPCHK(h, hipMemcpyAsync(st, h->ctl->mt, 625 * 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return 0;
 }
 
 int mdp_make_index(mdp_handle* h, int32_t count, int32_t* idx_dev) {
+  MDP_NEED(h);
   if (count < 0) return fail(h, "negative count");
   if (count == 0) return 0;
   return launch_make_index(h, count, idx_dev);
 }
 
 int mdp_sample_rows(mdp_handle* h, const int32_t* idx_dev, int32_t count, float* out_dev) {
+  MDP_NEED(h);
   if (count <= 0) return 0;
   ProfScope p(h, MDP_K_GATHER, false);
   HIPCHK(h, mdp_launch_gather(h->replay, h->L.topo.row_stride, idx_dev, count, out_dev, h->stream));
@@ -1623,6 +1646,7 @@ int mdp_q_values(mdp_handle* h, int32_t agent, int32_t target, const float* x_de
 
 // ---------------------------------------------------------------- training
 int mdp_update_gate(mdp_handle* h, int64_t t) {
+  MDP_NEED(h);
   if (h->len < (int64_t)h->cfg.batch_size * h->cfg.max_episode_len) return 1;  // maddpg.py:162-163
   if (t % 100 != 0) return 1;                                                   // maddpg.py:164-165
   return 0;
@@ -1642,7 +1666,7 @@ int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float
 
 int mdp_agent_update(mdp_handle* h, int32_t agent, int64_t t, const int32_t* idx_dev, const float* u_dev,
                      double stats_out[6]) {
-  if (!h || !stats_out) return -1;
+  if (unusable(h) || !stats_out) return -1;
   if (bad_agent(h, agent)) return -1;
   if (mdp_update_gate(h, t)) return 1;
   const float* u_tgt = u_dev;
@@ -1750,6 +1774,7 @@ static bool any_prof(const mdp_handle* h) {
 // control block), so the round is captured once and replayed with one
 // hipGraphLaunch.  Per-kernel event profiling runs the eager path.
 int mdp_update_round(mdp_handle* h) {
+  MDP_NEED(h);
   if (h->len <= 0) return fail(h, "update round on an empty replay buffer");
   if (!h->graphs || any_prof(h) || h->eager_rounds < 1) {
     ++h->eager_rounds;  // the first round runs eagerly (one-time kernel attribute setup)
@@ -1775,7 +1800,7 @@ int mdp_update_round(mdp_handle* h) {
 }
 
 int mdp_grad_variant(mdp_handle* h, int32_t agent) {
-  if (!h || agent < 0 || agent >= h->cfg.n_agents) return -1;
+  if (unusable(h) || agent < 0 || agent >= h->cfg.n_agents) return -1;
   return (!h->general_grads && grads_r_ok(h->L.topo, agent)) ? 1 : 0;
 }
 
@@ -1788,8 +1813,8 @@ int mdp_dp_unique_id(uint8_t* out128) {
 }
 
 int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank) {
-  if (h && h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
-  if (!h || !id128) return -1;
+  if (unusable(h) || !id128) return -1;
+  if (h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
   if (h->p2p || h->xbuf) return fail(h, "mdp_dp_init: the xGMI exchange is already set up");
   if (!rccl().ok) return fail(h, "librccl.so.1 could not be loaded");
   if (world < 1 || rank < 0 || rank >= world) return fail(h, "mdp_dp_init: bad world/rank");
@@ -1825,7 +1850,7 @@ int mdp_dp_init(mdp_handle* h, const uint8_t* id128, int32_t world, int32_t rank
 static void drop_graphs(mdp_handle* h);
 
 int mdp_dp_xgmi_open(mdp_handle* h, int32_t world, int32_t rank, uint8_t* handle_out) {
-  if (!h || !handle_out) return -1;
+  if (unusable(h) || !handle_out) return -1;
   if (h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
   if (h->comm) return fail(h, "mdp_dp_xgmi_open: an RCCL communicator is already set up");
   if (h->xbuf) return fail(h, "mdp_dp_xgmi_open: already open");
@@ -1854,7 +1879,7 @@ int mdp_dp_xgmi_open(mdp_handle* h, int32_t world, int32_t rank, uint8_t* handle
 }
 
 int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles) {
-  if (!h || !handles) return -1;
+  if (unusable(h) || !handles) return -1;
   if (!h->xbuf) return fail(h, "mdp_dp_xgmi_connect: call mdp_dp_xgmi_open first");
   if (!h->x_opened.empty()) return fail(h, "mdp_dp_xgmi_connect: already connected");
   const int W = h->x_world, r = h->x_rank;
@@ -1881,7 +1906,8 @@ int mdp_dp_xgmi_connect(mdp_handle* h, const uint8_t* handles) {
 }
 
 int mdp_dp_xgmi_probe(mdp_handle* h, int32_t* mismatches) {
-  if (!h || !h->xd_dev) return fail(h, "mdp_dp_xgmi_probe: not connected");
+  if (unusable(h)) return -1;
+  if (!h->xd_dev) return fail(h, "mdp_dp_xgmi_probe: not connected");
   const int nchunk = MDP_XCH_PROBE / 256;
   HIPCHK(h, hipMemsetAsync(h->x_probe, 0, 2 * sizeof(uint32_t), h->stream));
   for (int k = 0; k < 4; ++k)  // both slots, each reused once
@@ -1896,7 +1922,8 @@ int mdp_dp_xgmi_probe(mdp_handle* h, int32_t* mismatches) {
 }
 
 int mdp_dp_xgmi_enable(mdp_handle* h) {
-  if (!h || !h->xd_dev) return fail(h, "mdp_dp_xgmi_enable: not connected");
+  if (unusable(h)) return -1;
+  if (!h->xd_dev) return fail(h, "mdp_dp_xgmi_enable: not connected");
   if (h->update_mode != 0) return fail(h, "join data parallelism before choosing the throughput mode");
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->p2p = true;
@@ -1906,7 +1933,7 @@ int mdp_dp_xgmi_enable(mdp_handle* h) {
 }
 
 int mdp_dp_xgmi_close(mdp_handle* h) {
-  if (!h) return -1;
+  if (unusable(h)) return -1;
   (void)hipGetLastError();  // a failed open/map must not surface at the next launch check
   if (h->stream) HIPCHK(h, hipStreamSynchronize(h->stream));
   xgmi_release(h);
@@ -1916,7 +1943,7 @@ int mdp_dp_xgmi_close(mdp_handle* h) {
 }
 
 int mdp_dp_info(mdp_handle* h, int32_t out4[4]) {
-  if (!h || !out4) return -1;
+  if (unusable(h) || !out4) return -1;
   out4[0] = h->p2p ? 2 : (h->comm ? 1 : 0);
   out4[1] = 1;
   out4[2] = h->cfg.rank;
@@ -1935,7 +1962,7 @@ int mdp_dp_info(mdp_handle* h, int32_t out4[4]) {
 }
 
 int mdp_dp_exchange_stats(mdp_handle* h, double out4[4], int32_t reset) {
-  if (!h || !out4) return -1;
+  if (unusable(h) || !out4) return -1;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   uint64_t w[3] = {0, 0, 0};
   HIPCHK(h, hipMemcpy(w, &h->ctl->xw_ticks, sizeof(w), hipMemcpyDeviceToHost));
@@ -1952,12 +1979,13 @@ int mdp_dp_exchange_stats(mdp_handle* h, double out4[4], int32_t reset) {
 }
 
 int mdp_dp_exchange_stats_enable(mdp_handle* h, int32_t on) {
-  if (!h) return -1;
+  if (unusable(h)) return -1;
   h->xw_stats = on != 0;
   return 0;
 }
 
 int mdp_set_graphs(mdp_handle* h, int32_t on) {
+  MDP_NEED(h);
   h->graphs = on != 0;
   return 0;
 }
@@ -1980,7 +2008,7 @@ static void drop_graphs(mdp_handle* h) {
 }
 
 int mdp_set_update_mode(mdp_handle* h, int32_t mode) {
-  if (!h) return -1;
+  if (unusable(h)) return -1;
   if (mode != 0 && mode != 1) return fail(h, "update mode must be 0 (strict) or 1 (throughput)");
   if (mode == 1) {
     if (!tp_ok(h)) return fail(h, "throughput mode needs the fused optimizer step for every net and <= 8 agents");
@@ -1996,7 +2024,7 @@ int mdp_set_update_mode(mdp_handle* h, int32_t mode) {
 }
 
 int mdp_update_all(mdp_handle* h, const int32_t* idx_dev, const float* u_tgt_dev, const float* u_act_dev) {
-  if (!h) return -1;
+  if (unusable(h)) return -1;
   if (h->update_mode != 1) return fail(h, "mdp_update_all: set throughput mode first");
   if (h->len <= 0) return fail(h, "update on an empty replay buffer");
   const int32_t* idx = idx_dev;
@@ -2041,6 +2069,7 @@ int mdp_get_stats(mdp_handle* h, int32_t agent, double out6[6]) {
 
 // -------------------------------------------------------------------- env
 static int need_env(mdp_handle* h) {
+  MDP_NEED(h);
   if (h->cfg.scenario == MDP_SCN_NONE || h->cfg.num_envs <= 0) return fail(h, "handle has no device env");
   return 0;
 }
@@ -2309,6 +2338,7 @@ int mdp_env_obs(mdp_handle* h, float* obs_dev) {
 }
 
 int64_t mdp_episode_count(mdp_handle* h) {
+  MDP_NEED(h);
   int64_t n = 0;
   if (hipMemcpyAsync(&n, &h->ctl->episodes, 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess) return -1;
   if (hipStreamSynchronize(h->stream) != hipSuccess) return -1;
@@ -2316,6 +2346,7 @@ int64_t mdp_episode_count(mdp_handle* h) {
 }
 
 int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out) {
+  MDP_NEED(h);
   const int64_t cap = h->L.eplog_rows, w = 1 + h->cfg.n_agents;
   if (n > cap || first < 0) return fail(h, "episode log request exceeds ring");
   int64_t done = 0;
@@ -2331,6 +2362,7 @@ int mdp_episode_log(mdp_handle* h, int64_t first, int64_t n, float* out) {
 
 // -------------------------------------------------------------- profiling
 int mdp_prof_enable(mdp_handle* h, int32_t kind, int32_t on) {
+  MDP_NEED(h);
   if (kind < 0 || kind >= MDP_K_COUNT) return fail(h, "bad kernel kind");
   if (!on) flush_prof(h, kind);
   h->prof_on[kind] = on != 0;
@@ -2343,6 +2375,7 @@ int mdp_prof_enable(mdp_handle* h, int32_t kind, int32_t on) {
 }
 
 int mdp_prof_read(mdp_handle* h, int32_t kind, double* total_ms, int64_t* launches) {
+  MDP_NEED(h);
   if (kind < 0 || kind >= MDP_K_COUNT) return fail(h, "bad kernel kind");
   flush_prof(h, kind);
   if (total_ms) *total_ms = h->prof_ms[kind];
