@@ -1405,6 +1405,10 @@ int mdp_destroy(mdp_handle* h) {
   for (auto& kv : h->multi_exec) (void)hipGraphExecDestroy(kv.second);
   if (h->round_graph) (void)hipGraphDestroy(h->round_graph);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+#ifdef MDP_EXP_TPRE
+  if (h->tp_exp_topo) (void)hipFree(h->tp_exp_topo);
+  if (h->tp_exp_out) (void)hipFree(h->tp_exp_out);
+#endif
   delete h;
   return 0;
 }
