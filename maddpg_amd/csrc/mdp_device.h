@@ -34,6 +34,22 @@ __device__ __forceinline__ f32x4 mdp_mfma_x2(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(z, b, c, 0, 0, 0);
 }
 #define MDP_MFMA(a, b, c) mdp_mfma_x2((a), (b), (c))
+#elif defined(MDP_EXP_BF6) && defined(MDP_TU_GRADS_R)
+// timing-only build of the register-resident kernels (mdp_grads_r.hip): every
+// fp32 step issued as ONE bf16 v_mfma_f32_16x16x32_bf16
+// on a constant operand (16 cycles issue and dependent latency against the fp32
+// step's 32 / 40: the MFMA chains at 2x, a bound for an exact bf16x6 split,
+// tools/bf16x6_probe.hip, before its operand-split cost).  The step's own
+// operands are consumed by an empty asm, so their loads are waited for where
+// they are now.  Results are meaningless; never the shipped library.
+typedef __bf16 mdp_bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mdp_mfma_bf6(float a, float b, f32x4 c) {
+  asm volatile("" ::"v"(a), "v"(b));
+  const mdp_bf16x8 k = {(__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f,
+                        (__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f};
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(k, k, c, 0, 0, 0);
+}
+#define MDP_MFMA(a, b, c) mdp_mfma_bf6((a), (b), (c))
 #else
 #define MDP_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 #endif

@@ -34,6 +34,7 @@
 //   wave 0  da = dh1c W1c[a_i]^T, softmax backward + reg -> dlogits, d2a, dW3a, db3a | B5
 //   waves 0..3 dW2a (four tiles each, interleaved), db2a  ||  waves 4..7 dh1a tiles | B6
 //   all     dW1a, db1a
+#define MDP_TU_GRADS_R  // this translation unit (the MDP_EXP_BF6 timing build applies to it alone)
 #include "mdp_device.h"
 #include "mdp_kernels.h"
 #include "mdp_mt.h"
