@@ -40,3 +40,26 @@ def test_bench_json_line():
 def test_smoke():
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+def test_bench_two_ranks_driver_command_shape():
+    """The driver's N>1 command (torchrun, one rank per GPU, `--gpus N`) on this
+    one-GPU box: both ranks on cuda:0 (MDP_SHARED_GPU=1, a gloo group -- RCCL
+    refuses two ranks on one device), the real xGMI exchange between them.  One
+    JSON line from rank 0 with the whole-job value, and replicas bit-identical."""
+    import random
+    env = dict(os.environ, MDP_SHARED_GPU="1", MDP_DP_XGMI="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29400 + random.randrange(400)),
+           "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--num-envs", "256",
+           "--no-throughput-figure"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    dp = d["dp_check"]
+    assert dp["replicas_identical"] is True
+    assert dp["peers_per_rank"] == [1, 1]
