@@ -295,15 +295,6 @@ def configs2_per_gpu(args, steps=12, warmup=3):
     return out
 
 
-def _free_port():
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
 def rank_launch_plan(gpus, environ, argv, port=None):
     """How `bench.py --gpus N` becomes N ranks (pure host logic, tested on CPU).
 
@@ -325,8 +316,10 @@ def rank_launch_plan(gpus, environ, argv, port=None):
         return None
     if gpus == 1:
         return None
+    # the rendezvous store binds its own port (endpoint port 0: no probe-then-
+    # bind race with other jobs on a shared box); every address is 127.0.0.1
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-            "--master-addr", "127.0.0.1", "--master-port", str(port or _free_port()),
+            "--rdzv-backend=c10d", f"--rdzv-endpoint=127.0.0.1:{int(port or 0)}", "--local-addr", "127.0.0.1",
             os.path.join(ROOT, "bench.py")] + list(argv)
 
 

@@ -343,10 +343,6 @@ struct mdp_handle {
   bool rollout_draw = true;           // step_launches: first-round draw inside k_rollout
   bool draw_ahead = true;             // step_launches: draws one agent ahead (MDP_DRAW_AHEAD=0: per round)
   bool grad_pair = true;              // throughput mode, general kernels: critic + actor step in one launch (MDP_GRAD_PAIR=0: two)
-#ifdef MDP_EXP_TPRE
-  Topo* tp_exp_topo = nullptr;        // timing-only experiment: device copy of the topology
-  float* tp_exp_out = nullptr;        // ... and its a~ scratch [B][32]
-#endif
   // direct xGMI exchange (mdp_dp_p2p_*): this rank's IPC-exported buffer and
   // the device descriptor of every rank's buffer mapped here
   uint64_t* xbuf = nullptr;
@@ -385,6 +381,48 @@ bool unusable(const mdp_handle* h) { return !h || !h->ready; }
 #define MDP_NEED(h)               \
   do {                            \
     if (unusable(h)) return -1;   \
+  } while (0)
+
+// A caller buffer that a kernel dereferences ("_dev" in the header) must be
+// memory of the handle's device (hipMalloc, PyTorch's caching allocator,
+// managed memory) and hold `bytes` from `p` to the end of its allocation.  A
+// host address that reached a kernel faulted the GPU with an illegal memory
+// access instead of returning < 0 (round 5's r05h), so every entry
+// point checks its pointers here before anything is launched: one
+// hipPointerGetAttributes (+ hipMemGetAddressRange) per pointer, host-side
+// only; graph replays take no caller pointers.  null_ok: NULL means "not
+// given" for this argument.  h->device is set by mdp_create before any check.
+int need_dev(mdp_handle* h, const void* p, int64_t bytes, const char* fn, const char* arg, bool null_ok = true) {
+  auto refuse = [&](const char* why) {
+    std::string m = std::string(fn) + ": " + arg + " " + why;
+    return fail(h, m.c_str());
+  };
+  if (!p) return null_ok ? 0 : refuse("is null");
+  hipPointerAttribute_t a;
+  std::memset(&a, 0, sizeof(a));
+  const hipError_t e = hipPointerGetAttributes(&a, p);
+  // an unknown (host) address may set the runtime's last error: clear it, or
+  // the next launch's hipGetLastError check would report it
+  if (e != hipSuccess) (void)hipGetLastError();
+  const bool managed = a.isManaged || a.type == hipMemoryTypeManaged;
+  if (e != hipSuccess || !(a.type == hipMemoryTypeDevice || managed))
+    return refuse("is not device memory (a host address would fault the GPU); pass a buffer of the handle's device");
+  if (!managed && a.device != h->device) return refuse("is memory of another device than the handle's");
+  if (!managed && bytes > 0) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess) {
+      if ((const char*)p + bytes > (const char*)base + size)
+        return refuse("ends before the bytes this call reads or writes (allocation too small)");
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  return 0;
+}
+#define MDP_DEV(h, p, bytes, fn, null_ok)                                   \
+  do {                                                                     \
+    if (need_dev(h, p, (int64_t)(bytes), fn, #p, null_ok)) return -1;     \
   } while (0)
 
 }  // namespace
@@ -649,11 +687,7 @@ ApplyArgs apply_args(mdp_handle* h, int agent, int net, float scale, bool tp = f
   chunks(a.other, a.oblk);
   a.slab = nullptr;
   a.slab_stride = net ? h->L.slab_c : h->L.slab_a;
-#ifdef MDP_EXP_R32  // timing-only build: 32-row gradient workgroups leave half the partials
-  a.nwg = (h->L.nwg + 1) / 2;
-#else
   a.nwg = h->L.nwg;
-#endif
   a.scale = scale;
   a.clip = h->cfg.grad_clip;
   a.lr = h->cfg.lr;
@@ -714,9 +748,6 @@ FusedApplyArgs fused_args_for(mdp_handle* h, int agent, int net, bool tp = false
   f.pf_count = 0;
   f.pf_out = nullptr;
   f.pf_ctl = h->ctl;
-#ifdef MDP_EXP_TPRE
-  f.tp_count = 0;
-#endif
   return f;
 }
 
@@ -752,21 +783,6 @@ int do_reduce_apply(mdp_handle* h, int agent, int net, int32_t* pf_out = nullptr
     f.pf_out = pf_out;
     f.pf_count = pf_count;
   }
-#ifdef MDP_EXP_TPRE  // timing only: the next agent's target-actor forwards on the idle CUs
-  if (h->tp_exp_topo && h->L.topo.H == 128 && h->cfg.n_agents > 1 && h->update_mode == 0) {
-    const int half = (h->L.nwg + 1) / 2;
-    f.tp_count = net ? half : (int)h->L.nwg - half;
-    f.tp_agent = (agent + 1) % h->cfg.n_agents;
-    f.tp_skip = agent;
-    f.tp_B = h->cfg.batch_size;
-    f.tp_topo = h->tp_exp_topo;
-    f.tp_replay = h->replay;
-    f.tp_target = h->target;
-    f.tp_idx = h->index;
-    f.tp_seed = h->cfg.seed;
-    f.tp_out = h->tp_exp_out;
-  }
-#endif
   if (h->p2p) set_xchg(h, f, agent, net);
   ProfScope p(h, MDP_K_REDUCE_APPLY);
   HIPCHK(h, mdp_launch_reduce_apply(f, h->stream));
@@ -1208,7 +1224,9 @@ int launch_tp_batch(mdp_handle* h, int ph) {
 // general path's optimizer launches
 int do_round_tp(mdp_handle* h, const int32_t* idx, const float* u_tgt, const float* u_act, int32_t* pf_out,
                 int32_t* draw_out = nullptr) {
-  if (!tp_fast(h)) return tp_round_general(h, idx, u_tgt, u_act, draw_out);
+  // the general path draws in its pair launches; a pf_out handed here anyway is
+  // filled there in the same MT19937 order (agent i's B at pf_out + i B)
+  if (!tp_fast(h)) return tp_round_general(h, idx, u_tgt, u_act, draw_out ? draw_out : pf_out);
   const int rc = tp_grads_fast(h, idx, u_tgt, u_act, pf_out);
   if (rc) return rc;
   if (h->p2p) {  // data parallel over xGMI: reduce + exchange + step of every net, one launch
@@ -1301,6 +1319,7 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
   }
   *out = h;
   HIPCHK(h, hipGetDevice(&h->device));
+  if (need_dev(h, arena_dev, h->L.total, "mdp_create", "arena_dev", false)) return -1;
   {
     int cus = 0, per = 0, per_b = 0;
     HIPCHK(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
@@ -1381,11 +1400,6 @@ int mdp_create(const mdp_config* cfg, void* arena_dev, int64_t arena_bytes, void
   std::memset(&c, 0, sizeof(c));
   py_seed_state(0, c.mt, &c.mt_pos);
   HIPCHK(h, hipMemcpyAsync(h->ctl, &c, sizeof(c), hipMemcpyHostToDevice, h->stream));
-#ifdef MDP_EXP_TPRE
-  HIPCHK(h, hipMalloc((void**)&h->tp_exp_topo, sizeof(Topo)));
-  HIPCHK(h, hipMemcpyAsync(h->tp_exp_topo, &h->L.topo, sizeof(Topo), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMalloc((void**)&h->tp_exp_out, sizeof(float) * 32 * (size_t)cfg->batch_size));
-#endif
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->err.clear();
   h->ready = true;
@@ -1405,10 +1419,6 @@ int mdp_destroy(mdp_handle* h) {
   for (auto& kv : h->multi_exec) (void)hipGraphExecDestroy(kv.second);
   if (h->round_graph) (void)hipGraphDestroy(h->round_graph);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
-#ifdef MDP_EXP_TPRE
-  if (h->tp_exp_topo) (void)hipFree(h->tp_exp_topo);
-  if (h->tp_exp_out) (void)hipFree(h->tp_exp_out);
-#endif
   delete h;
   return 0;
 }
@@ -1517,6 +1527,7 @@ int mdp_buffer_add_rows(mdp_handle* h, const float* rows_dev, int64_t rows) {
   MDP_NEED(h);
   if (rows < 0) return fail(h, "negative row count");
   if (rows == 0) return 0;
+  MDP_DEV(h, rows_dev, rows * 4 * h->L.topo.row_stride, "mdp_buffer_add_rows", false);
   const int64_t cap = h->cfg.capacity;
   // more rows than the ring holds: only the last `cap` survive (earlier ones
   // would be overwritten), which also keeps every destination row unique
@@ -1530,6 +1541,8 @@ int mdp_buffer_add_rows(mdp_handle* h, const float* rows_dev, int64_t rows) {
 int mdp_buffer_put_agent(mdp_handle* h, int32_t agent, const int64_t* pos_dev, const float* cols_dev, int64_t rows) {
   if (bad_agent(h, agent)) return -1;
   if (rows <= 0) return 0;
+  MDP_DEV(h, pos_dev, rows * 8, "mdp_buffer_put_agent", false);
+  MDP_DEV(h, cols_dev, rows * 4 * (2 * h->L.topo.ag[agent].obs_dim + MDP_ACT_DIM + 2), "mdp_buffer_put_agent", false);
   HIPCHK(h, mdp_launch_put_agent(h->replay, h->L.topo.row_stride, h->L.topo.ag[agent], pos_dev, cols_dev, rows,
                                  h->stream));
   return 0;
@@ -1574,12 +1587,15 @@ int mdp_make_index(mdp_handle* h, int32_t count, int32_t* idx_dev) {
   MDP_NEED(h);
   if (count < 0) return fail(h, "negative count");
   if (count == 0) return 0;
+  MDP_DEV(h, idx_dev, 4 * (int64_t)count, "mdp_make_index", false);
   return launch_make_index(h, count, idx_dev);
 }
 
 int mdp_sample_rows(mdp_handle* h, const int32_t* idx_dev, int32_t count, float* out_dev) {
   MDP_NEED(h);
   if (count <= 0) return 0;
+  MDP_DEV(h, idx_dev, 4 * (int64_t)count, "mdp_sample_rows", false);
+  MDP_DEV(h, out_dev, 4 * (int64_t)count * h->L.topo.row_stride, "mdp_sample_rows", false);
   ProfScope p(h, MDP_K_GATHER, false);
   HIPCHK(h, mdp_launch_gather(h->replay, h->L.topo.row_stride, idx_dev, count, out_dev, h->stream));
   return 0;
@@ -1591,6 +1607,9 @@ int mdp_act(mdp_handle* h, int32_t agent, int32_t target, const float* obs_dev, 
   if (bad_agent(h, agent)) return -1;
   if (rows <= 0) return 0;
   const ADesc& ag = h->L.topo.ag[agent];
+  MDP_DEV(h, obs_dev, 4 * (int64_t)rows * ag.obs_dim, "mdp_act", false);
+  MDP_DEV(h, act_dev, 4 * (int64_t)rows * MDP_ACT_DIM, "mdp_act", false);
+  MDP_DEV(h, u_dev, 4 * (int64_t)rows * MDP_ACT_DIM, "mdp_act", true);
   EvalArgs a;
   a.P = target ? h->target : h->theta;
   a.net = ag.actor;
@@ -1612,6 +1631,8 @@ int mdp_actor_logits(mdp_handle* h, int32_t agent, int32_t target, const float* 
   if (bad_agent(h, agent)) return -1;
   if (rows <= 0) return 0;
   const ADesc& ag = h->L.topo.ag[agent];
+  MDP_DEV(h, obs_dev, 4 * (int64_t)rows * ag.obs_dim, "mdp_actor_logits", false);
+  MDP_DEV(h, logits_dev, 4 * (int64_t)rows * MDP_ACT_DIM, "mdp_actor_logits", false);
   EvalArgs a;
   a.P = target ? h->target : h->theta;
   a.net = ag.actor;
@@ -1632,6 +1653,8 @@ int mdp_q_values(mdp_handle* h, int32_t agent, int32_t target, const float* x_de
   if (bad_agent(h, agent)) return -1;
   if (rows <= 0) return 0;
   const ADesc& ag = h->L.topo.ag[agent];
+  MDP_DEV(h, x_dev, 4 * (int64_t)rows * ag.cin, "mdp_q_values", false);
+  MDP_DEV(h, q_dev, 4 * (int64_t)rows, "mdp_q_values", false);
   EvalArgs a;
   a.P = target ? h->target : h->theta;
   a.net = ag.critic;
@@ -1658,6 +1681,10 @@ int mdp_update_gate(mdp_handle* h, int64_t t) {
 
 int mdp_update(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev, const float* u_act_dev) {
   if (bad_agent(h, agent)) return -1;
+  const int64_t B = h->cfg.batch_size, n = h->cfg.n_agents;
+  MDP_DEV(h, idx_dev, 4 * B, "mdp_update", true);
+  MDP_DEV(h, u_tgt_dev, 4 * n * B * MDP_ACT_DIM, "mdp_update", true);
+  MDP_DEV(h, u_act_dev, 4 * B * MDP_ACT_DIM, "mdp_update", true);
   const int32_t* idx = idx_dev;
   if (!idx) {
     int32_t* slot = h->index + (int64_t)agent * h->cfg.batch_size;
@@ -1673,6 +1700,7 @@ int mdp_agent_update(mdp_handle* h, int32_t agent, int64_t t, const int32_t* idx
   if (unusable(h) || !stats_out) return -1;
   if (bad_agent(h, agent)) return -1;
   if (mdp_update_gate(h, t)) return 1;
+  MDP_DEV(h, u_dev, 4 * (int64_t)(h->cfg.n_agents + 1) * h->cfg.batch_size * MDP_ACT_DIM, "mdp_agent_update", true);
   const float* u_tgt = u_dev;
   const float* u_act = u_dev ? u_dev + (int64_t)h->cfg.n_agents * h->cfg.batch_size * MDP_ACT_DIM : nullptr;
   const int rc = mdp_update(h, agent, idx_dev, u_tgt, u_act);
@@ -2031,6 +2059,12 @@ int mdp_update_all(mdp_handle* h, const int32_t* idx_dev, const float* u_tgt_dev
   if (unusable(h)) return -1;
   if (h->update_mode != 1) return fail(h, "mdp_update_all: set throughput mode first");
   if (h->len <= 0) return fail(h, "update on an empty replay buffer");
+  {
+    const int64_t B = h->cfg.batch_size, n = h->cfg.n_agents;
+    MDP_DEV(h, idx_dev, 4 * n * B, "mdp_update_all", true);
+    MDP_DEV(h, u_tgt_dev, 4 * n * n * B * MDP_ACT_DIM, "mdp_update_all", true);
+    MDP_DEV(h, u_act_dev, 4 * n * B * MDP_ACT_DIM, "mdp_update_all", true);
+  }
   const int32_t* idx = idx_dev;
   if (!idx) {
     const int rc = launch_make_index(h, h->cfg.n_agents * h->cfg.batch_size, h->index);
@@ -2043,12 +2077,16 @@ int mdp_update_all(mdp_handle* h, const int32_t* idx_dev, const float* u_tgt_dev
 int mdp_critic_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_tgt_dev) {
   if (bad_agent(h, agent)) return -1;
   if (!idx_dev) return fail(h, "critic_grad needs indices");
+  MDP_DEV(h, idx_dev, 4 * (int64_t)h->cfg.batch_size, "mdp_critic_grad", false);
+  MDP_DEV(h, u_tgt_dev, 4 * (int64_t)h->cfg.n_agents * h->cfg.batch_size * MDP_ACT_DIM, "mdp_critic_grad", true);
   return do_critic_grad(h, agent, idx_dev, u_tgt_dev);
 }
 
 int mdp_actor_grad(mdp_handle* h, int32_t agent, const int32_t* idx_dev, const float* u_act_dev) {
   if (bad_agent(h, agent)) return -1;
   if (!idx_dev) return fail(h, "actor_grad needs indices");
+  MDP_DEV(h, idx_dev, 4 * (int64_t)h->cfg.batch_size, "mdp_actor_grad", false);
+  MDP_DEV(h, u_act_dev, 4 * (int64_t)h->cfg.batch_size * MDP_ACT_DIM, "mdp_actor_grad", true);
   return do_actor_grad(h, agent, idx_dev, u_act_dev);
 }
 
@@ -2137,6 +2175,9 @@ static void advance_ring_mirror(mdp_handle* h) {
 
 int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
   if (need_env(h)) return -1;
+  const int64_t en5 = 4 * (int64_t)h->cfg.num_envs * h->cfg.n_agents * MDP_ACT_DIM;
+  MDP_DEV(h, act_in_dev, en5, "mdp_env_step", true);
+  MDP_DEV(h, u_dev, en5, "mdp_env_step", true);
   const int rc = env_step_launch(h, act_in_dev, u_dev);
   if (rc) return rc;
   advance_ring_mirror(h);
@@ -2146,6 +2187,7 @@ int mdp_env_step(mdp_handle* h, const float* act_in_dev, const float* u_dev) {
 int mdp_env_step_bench(mdp_handle* h, float* info_dev) {
   if (need_env(h)) return -1;
   if (!info_dev) return fail(h, "mdp_env_step_bench: info_dev is null");
+  MDP_DEV(h, info_dev, 4 * (int64_t)h->cfg.num_envs * h->cfg.n_agents * MDP_BENCH_W, "mdp_env_step_bench", false);
   if (h->cfg.scenario == MDP_SCN_SIMPLE)
     return fail(h, "scenario 'simple' has no benchmark_data (MPE Scenario attribute missing)");
   const int rc = env_step_launch(h, nullptr, nullptr, info_dev);
@@ -2161,7 +2203,10 @@ int mdp_env_step_bench(mdp_handle* h, float* info_dev) {
 static int step_launches(mdp_handle* h, int rounds) {
   const int nb = h->cfg.n_agents * h->cfg.batch_size;
   int32_t* slot[2] = {h->index, h->index + nb};
-  const bool pf = prefetch_ok(h);
+  // the critic-launch prefetch serves throughput mode only where its one critic
+  // launch covers every agent (tp_fast); a mix of fast and general agents
+  // (e.g. tag with DDPG adversaries) draws in the optimizer pair launches
+  const bool pf = prefetch_ok(h) && (h->update_mode == 0 || tp_fast(h));
   // (throughput mode on the general kernels: in its optimizer pair launches, RCCL included)
   const bool ra_draw = !pf && (h->update_mode == 0 ? draw_in_ra_ok(h) : !tp_fast(h));
   bool fast_all = !h->general_grads;
@@ -2329,6 +2374,11 @@ int mdp_env_set_state(mdp_handle* h, const float* pos, const float* vel, const i
 
 int mdp_env_obs(mdp_handle* h, float* obs_dev) {
   if (need_env(h)) return -1;
+  {
+    int64_t so = 0;
+    for (int i = 0; i < h->cfg.n_agents; ++i) so += h->cfg.obs_dim[i];
+    MDP_DEV(h, obs_dev, 4 * (int64_t)h->cfg.num_envs * so, "mdp_env_obs", false);
+  }
   EnvObsArgs a;
   a.topo = h->L.topo;
   a.env = h->L.env;

@@ -558,75 +558,6 @@ extern "C" int mdp_debug_ra_wg(unsigned long long* t0, unsigned long long* t1, i
   } while (0)
 #endif
 
-#ifdef MDP_EXP_TPRE
-#include "mdp_queue.h"
-// timing-only: the target-actor forwards of the next agent's critic step (all
-// target actors but tp_skip) over 16 rows of its batch, as extra workgroups of
-// an optimizer launch (the bound of running them on the CUs the chunk
-// workgroups leave idle)
-template <int H>
-__device__ __forceinline__ void tpre_role(const FusedApplyArgs& f, int tile) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Topo& T = *f.tp_topo;
-  const int ldr = lds_ld(T.row_stride), ldh = H + 1, S = MDP_R * ldh;
-  const int na = T.n - 1;  // (LDS: 16 x row + 2 x 5 x 16 x 129 + logits ~ 104 KB at tag N = 6)
-  LdsCarve cv(lds);
-  float* rowbuf = cv.take(MDP_R * ldr);
-  float* hA = cv.take(na * S);
-  float* hB = cv.take(na * S);
-  float* lg = cv.take(na * MDP_R * 8);
-  int* cnt = reinterpret_cast<int*>(cv.take(MDP_MAX_AGENTS + 4));
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
-  const int r0 = (tile * MDP_R) % f.tp_B;
-  const int nvalid = min(MDP_R, f.tp_B - r0);
-  const uint32_t ctr = f.ap.ctl->upd_ctr + 1u;
-  gather_rows16(f.tp_replay, T.row_stride, f.tp_idx, r0, nvalid, rowbuf, ldr);
-  if (tid < MDP_MAX_AGENTS + 4) cnt[tid] = 0;
-  __syncthreads();
-  const int o_row = (int)(rowbuf - lds), o_ha = (int)(hA - lds), o_hb = (int)(hB - lds);
-  auto jobf = [&](int layer, int jb) -> TileJob {
-    const int j = jb < f.tp_skip ? jb : jb + 1;
-    const ADesc& aj = T.ag[j];
-    const NDesc& net = aj.actor;
-    TileJob t;
-    t.k0 = 0;
-    if (layer == 0) {
-      t.xoff = o_row + aj.nobs_off;
-      t.ldx = ldr;
-      t.K = aj.obs_dim;
-      t.W = f.tp_target + net.t[0].off;
-      t.b = f.tp_target + net.t[1].off;
-      t.yoff = o_ha + jb * S;
-    } else {
-      t.xoff = o_ha + jb * S;
-      t.ldx = ldh;
-      t.K = H;
-      t.W = f.tp_target + net.t[2].off;
-      t.b = f.tp_target + net.t[3].off;
-      t.yoff = o_hb + jb * S;
-    }
-    return t;
-  };
-  fwd_phase_l12(lds, na, na, H, ldh, cnt, cnt + MDP_MAX_AGENTS + 3, H >> 6, jobf, [](int q) { return q; });
-  __syncthreads();
-  for (int jb = wave; jb < na; jb += nw) {
-    const int j = jb < f.tp_skip ? jb : jb + 1;
-    const NDesc& an = T.ag[j].actor;
-    head_mfma<H / 4>(hB + jb * S, ldh, H, f.tp_target + an.t[4].off, f.tp_target + an.t[5].off, MDP_ACT_DIM,
-                     lg + jb * MDP_R * 8, 8);
-  }
-  __syncthreads();
-  for (int e = tid; e < na * MDP_R; e += blockDim.x) {
-    const int jb = e / MDP_R, row = e - jb * MDP_R;
-    const int j = jb < f.tp_skip ? jb : jb + 1;
-    float u[MDP_ACT_DIM], act[MDP_ACT_DIM];
-    uniforms5(f.tp_seed, (uint32_t)((f.tp_agent << 8) | (j + 1)), ctr, (uint32_t)(r0 + row), u);
-    gumbel_softmax5(lg + jb * MDP_R * 8 + row * 8, u, act);
-    if (row < nvalid)
-      for (int k = 0; k < MDP_ACT_DIM; ++k) f.tp_out[(int64_t)(r0 + row) * 32 + MDP_ACT_DIM * j + k] = act[k];
-  }
-}
-#endif
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_reduce_apply(FusedApplyArgs f) {
@@ -641,18 +572,7 @@ __global__ __launch_bounds__(NT) void k_reduce_apply(FusedApplyArgs f) {
     MDP_RA_WG(g_ra_t1);
     return;
   }
-#ifdef MDP_EXP_TPRE
-  if constexpr (NT == 1024) {
-    const int ra = f.rblk[6] + (f.ap.polyak ? f.ap.oblk[6] : 0) + (f.ap.stats_mode ? 1 : 0);
-    if (f.tp_count > 0 && (int)blockIdx.x >= ra) {
-      tpre_role<128>(f, blockIdx.x - ra);
-      return;
-    }
-  }
-  reduce_apply_body<NT / 64>(f, blockIdx.x, gridDim.x - (f.pf_count > 0 ? 1 : 0) - f.tp_count);
-#else
   reduce_apply_body<NT / 64>(f, blockIdx.x, gridDim.x - (f.pf_count > 0 ? 1 : 0));
-#endif
 #ifdef MDP_STAMPS
   __syncthreads();
   MDP_RA_WG(g_ra_t1);
@@ -688,20 +608,6 @@ int mdp_ra_grid(const FusedApplyArgs& f) {
 static bool mdp_ra_narrow(const FusedApplyArgs& f) { return MDP_RA_NARROW && f.ap.nwg <= 64; }
 
 hipError_t mdp_launch_reduce_apply(const FusedApplyArgs& f, hipStream_t s) {
-#ifdef MDP_EXP_TPRE
-  if (f.tp_count > 0 && !mdp_ra_narrow(f)) {
-    static bool attr = false;
-    if (!attr) {
-      // (the dynamic size itself: the kernel's ~20 KB of static LDS count against the 160 KB)
-      (void)hipFuncSetAttribute((const void*)k_reduce_apply<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                108 * 1024);
-      attr = true;
-    }
-    const dim3 grid(mdp_ra_grid(f) + f.tp_count + (f.pf_count > 0 ? 1 : 0));
-    mdp_launch(k_reduce_apply<1024>, grid, dim3(1024), 108 * 1024, s, f);
-    return hipGetLastError();
-  }
-#endif
   const dim3 grid(mdp_ra_grid(f) + (f.pf_count > 0 ? 1 : 0));
   if (mdp_ra_narrow(f))
     mdp_launch(k_reduce_apply<256>, grid, dim3(256), 0, s, f);

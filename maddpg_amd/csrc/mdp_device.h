@@ -21,38 +21,9 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // one fp32 MFMA step, D = A x B + C over a 16x16 tile with k = 4 (exact fp32:
-// the bitwise fmaf chain, MI355X_MICROARCH.md).  MDP_EXP_R32 (timing-only
-// build of the register-resident kernels, tools/build_variant.sh): every step
-// is issued a second time with an opaque zero A operand into the same
-// accumulator -- the MFMA work of a 32-row tile on the same weight fragment,
-// results unchanged (0 x b + c == c) -- to size 32-row workgroups at S2
-#ifdef MDP_EXP_R32
-__device__ __forceinline__ f32x4 mdp_mfma_x2(float a, float b, f32x4 c) {
-  float z = 0.f;
-  asm volatile("" : "+v"(z));
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(z, b, c, 0, 0, 0);
-}
-#define MDP_MFMA(a, b, c) mdp_mfma_x2((a), (b), (c))
-#elif defined(MDP_EXP_BF6) && defined(MDP_TU_GRADS_R)
-// timing-only build of the register-resident kernels (mdp_grads_r.hip): every
-// fp32 step issued as ONE bf16 v_mfma_f32_16x16x32_bf16
-// on a constant operand (16 cycles issue and dependent latency against the fp32
-// step's 32 / 40: the MFMA chains at 2x, a bound for an exact bf16x6 split,
-// tools/bf16x6_probe.hip, before its operand-split cost).  The step's own
-// operands are consumed by an empty asm, so their loads are waited for where
-// they are now.  Results are meaningless; never the shipped library.
-typedef __bf16 mdp_bf16x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ f32x4 mdp_mfma_bf6(float a, float b, f32x4 c) {
-  asm volatile("" ::"v"(a), "v"(b));
-  const mdp_bf16x8 k = {(__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f,
-                        (__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f, (__bf16)1e-3f};
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(k, k, c, 0, 0, 0);
-}
-#define MDP_MFMA(a, b, c) mdp_mfma_bf6((a), (b), (c))
-#else
+// the bitwise fmaf chain, MI355X_MICROARCH.md).  (Timing-only variants of
+// this step live in tools/variants/mdp_exp.patch, not in the product.)
 #define MDP_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
-#endif
 
 // diagnostic build only (-DMDP_STAMPS): wall-clock stamps of workgroup 0
 #ifdef MDP_STAMPS

@@ -405,11 +405,7 @@ __device__ __forceinline__ void critic_body(const CriticArgs& a, const Topo& T, 
 
   // target actors of the group (+ the critic forward with the first group): each
   // layer phase deals every net's 16-column tiles over all waves
-#ifdef MDP_EXP_ONE_TACT  // timing only: ONE target actor in the launch (the bound of hoisting the other n - 1)
-  const int nact = (lq || a.B > 0) ? 1 : T.n;  // (a run-time 1: a compile-time one re-shaped the kernel into 2 KB of spills)
-#else
   const int nact = lq ? 1 : T.n;
-#endif
   const int npass = (nact + G - 1) / G;
   // the target critic's obs' part of layer 1 (maddpg.py:86) does not depend on
   // the target actions: with the first layer-1 phase, raw, into xl (unused by a
@@ -497,23 +493,9 @@ __device__ __forceinline__ void critic_body(const CriticArgs& a, const Topo& T, 
     };
     if (!sp && H >= 128) {  // layer 1 + layer 2 as one phase, per-net hand-off (fwd_phase_l12; at H = 64 it spills)
       // layer-1 order: the long jobs first (critic, the target critic's obs' part), then the actors
-#ifdef MDP_EXP_NO_CRITQ  // timing only: the critic forward and the target critic's obs' part out of the queue
-      // (the bound of computing them ahead, in the previous agent's launches); finite stand-ins
-      const bool skipc = g0 == 0 && a.B > 0;  // (run-time: a compile-time constant re-shapes the kernel)
-      if (skipc)
-        for (int e = tid; e < MDP_R * ldh; e += blockDim.x) {
-          h1c[e] = 0.05f;
-          h2c[e] = 0.05f;
-          if (tpre) xl[e] = 0.01f;
-        }
-      const int nlong = skipc ? 0 : nj1 - ng;
-      fwd_phase_l12(lds, skipc ? ng : nj1, skipc ? ng : nj, H, ldh, cnt, cnt + MDP_MAX_AGENTS + 3,
-                    (H >> 6) * (pass + 1), jobf, [&](int q) { return q < nlong ? ng + q : q - nlong; });
-#else
       const int nlong = nj1 - ng;
       fwd_phase_l12(lds, nj1, nj, H, ldh, cnt, cnt + MDP_MAX_AGENTS + 3, (H >> 6) * (pass + 1), jobf,
                     [&](int q) { return q < nlong ? ng + q : q - nlong; });
-#endif
       if (g0 == 0) MDP_STAMPW(16 + wave);  // per-wave phase end (diagnostic build)
       __syncthreads();
       if (tid == 0) cnt[MDP_MAX_AGENTS + 3] = 0;  // the queue of the next group (barriers follow)
@@ -570,10 +552,6 @@ __device__ __forceinline__ void critic_body(const CriticArgs& a, const Topo& T, 
       const int dst = lq ? ag.obs_dim : T.sum_obs + MDP_ACT_DIM * j;
       for (int k = 0; k < MDP_ACT_DIM; ++k) xt[row * ldc + dst + k] = act[k];
     }
-#ifdef MDP_EXP_ONE_TACT  // (the skipped actors' a~ columns: a finite stand-in)
-    for (int e = tid; e < MDP_R * MDP_ACT_DIM * (T.n - 1); e += blockDim.x)
-      xt[(e / (MDP_ACT_DIM * (T.n - 1))) * ldc + T.sum_obs + MDP_ACT_DIM + e % (MDP_ACT_DIM * (T.n - 1))] = 0.2f;
-#endif
     __syncthreads();
   }
   MDP_STAMP(2);

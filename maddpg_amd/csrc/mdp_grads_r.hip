@@ -34,18 +34,12 @@
 //   wave 0  da = dh1c W1c[a_i]^T, softmax backward + reg -> dlogits, d2a, dW3a, db3a | B5
 //   waves 0..3 dW2a (four tiles each, interleaved), db2a  ||  waves 4..7 dh1a tiles | B6
 //   all     dW1a, db1a
-#define MDP_TU_GRADS_R  // this translation unit (the MDP_EXP_BF6 timing build applies to it alone)
 #include "mdp_device.h"
 #include "mdp_kernels.h"
 #include "mdp_mt.h"
 
-// row tiles per workgroup for the grid: 16 rows (MDP_R); the timing-only
-// MDP_EXP_R32 build sizes 32-row workgroups (half the grid, see MDP_MFMA)
-#ifdef MDP_EXP_R32
-#define MDP_RW 32
-#else
+// row tiles per workgroup for the grid: 16 rows (MDP_R)
 #define MDP_RW MDP_R
-#endif
 
 // diagnostic build: every workgroup's start (wave 0) and per-wave end of the
 // last critic (k = 0) / actor (k = 1) launch -- which role ends the launch
@@ -776,9 +770,6 @@ __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
     // and needed late); waves 0..3 start on their weight loads at once
     if (post) load_rows16_part(a.cpre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 256, 256);
     else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 256, 256);
-#ifdef MDP_EXP_R32  // the second 16-row tile's rows (timing only: same buffer)
-    gather_rows16_part(a.replay, T.row_stride, idx, min(r0 + MDP_R, a.B - MDP_R), MDP_R, rowbuf, ldr, 256, 256);
-#endif
     lds_signal(&rows_ready);
 #ifdef MDP_STAMPS
     if (tt == 0) {
@@ -1046,9 +1037,6 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
       if (wave > 1) {
         if (a.apre) load_rows16_part(a.apre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 128, 384);
         else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
-#ifdef MDP_EXP_R32
-        gather_rows16_part(a.replay, T.row_stride, idx, min(r0 + MDP_R, a.B - MDP_R), MDP_R, rowbuf, ldr, 128, 384);
-#endif
       }
       if (wave > 1) lds_signal(&rows_ready);
       const int k0 = KC * (wave - 1);  // this wave's third of the replay-part contraction
@@ -1111,9 +1099,6 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
     // waves 2..7 gather the replay rows (first); waves 0, 1 start on their weights at once
     if (a.apre) load_rows16_part(a.apre_rows + (int64_t)r0 * T.row_stride, T.row_stride, rowbuf, ldr, 128, 384);
     else gather_rows16_part(a.replay, T.row_stride, idx, r0, nvalid, rowbuf, ldr, 128, 384);
-#ifdef MDP_EXP_R32
-    gather_rows16_part(a.replay, T.row_stride, idx, min(r0 + MDP_R, a.B - MDP_R), MDP_R, rowbuf, ldr, 128, 384);
-#endif
     lds_signal(&rows_ready);
     f32x4 wc[4], wa[4];
     lds_wait(&fwd_issued, 4);  // the critic forward's loads go first

@@ -188,18 +188,6 @@ struct FusedApplyArgs {
   int32_t* pf_out;
   Ctl* pf_ctl;
   ApplyArgs ap;         // ap.slab / nwg / slab_stride: the partial gradients
-#ifdef MDP_EXP_TPRE
-  // timing-only experiment: tp_count extra workgroups (before the draw piece) run
-  // the forwards of the target actors j != tp_skip over 16 rows each of agent
-  // tp_agent's batch (tp_idx) and store the sampled a~ into tp_out [B][32]
-  int tp_count, tp_agent, tp_skip, tp_B;
-  const Topo* tp_topo;
-  const float* tp_replay;
-  const float* tp_target;
-  const int32_t* tp_idx;
-  uint64_t tp_seed;
-  float* tp_out;
-#endif
 };
 // sync area: per (agent, net) 8 counters x 128 B (6 done, 7 norm epoch), then [6][MAXCH][2] tagged words
 inline int64_t mdp_ra_sync_bytes() {

@@ -1,8 +1,7 @@
 // mdp_queue.h -- the weight-chunk stream of the general (H >= 64) layer phases:
 // TileJob, rg_load / rg_acc (one 16-B load per lane and k-row feeding 4 MFMA
 // tiles) and fwd_phase_l12 (layer 1 + layer 2 of independent nets as one
-// work-queue phase).  Shared by mdp_grads.hip (the gradient kernels) and the
-// optimizer kernel's timing-only pre role (MDP_EXP_TPRE).
+// work-queue phase), used by mdp_grads.hip (the gradient kernels).
 #pragma once
 #include "mdp_device.h"
 
@@ -37,14 +36,7 @@ __device__ __forceinline__ void rg_load(f32x4 (&w)[KS], const float* __restrict_
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k = c0 + 4 * s + kq;
-#ifdef MDP_EXP_NOLOAD  // timing only: the grouped phases without their weight stream
-    w[s] = f32x4{1e-3f * (float)(k & 7), 1e-3f, 0.f, -1e-3f};
-    (void)W;
-    (void)N;
-    (void)col4;
-#else
     w[s] = *reinterpret_cast<const f32x4*>(W + (int64_t)min(k, K - 1) * N + col4);
-#endif
   }
 }
 template <int KS>
@@ -61,13 +53,8 @@ __device__ __forceinline__ void rg_acc(f32x4 (&acc)[4], const float* X, int ldx,
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if (c0 + 4 * s < K) {  // wave-uniform
-#ifdef MDP_EXP_NOMFMA  // timing only: the grouped phases' weight stream without their MFMAs
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t][t] += x[s] * w[s][t];
-#else
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], w[s][t], acc[t], 0, 0, 0);
-#endif
     }
   }
 }

@@ -19,6 +19,18 @@ from ._lib import MdpConfig, MdpTensorInfo
 TENSOR_NAMES = ("W1", "b1", "W2", "b2", "W3", "b3")
 
 
+
+# the dtypes of update()'s return value in the reference (maddpg.py:196):
+# q_loss, p_loss are the fp32 scalars U.function fetches from TF1 (:91, :54-56);
+# np.mean(target_q_next) is the mean of an fp32 array (fp32, :185); the mean
+# and std of the fp64 TD target and the mean reward are float64 (:186)
+UPDATE_STAT_DTYPES = (np.float32, np.float32, np.float64, np.float64, np.float32, np.float64)
+
+
+def update_stats(vals):
+    """the 6 device stats (fp64, mdp_get_stats) as the reference's list of numpy scalars"""
+    return [dt(v) for dt, v in zip(UPDATE_STAT_DTYPES, list(vals))]
+
 class Engine:
     def __init__(self, obs_dims, local_q=None, *, num_units=64, batch_size=1024, max_episode_len=25,
                  capacity=int(1e6), num_envs=0, scenario="none", num_adversaries=0, lr=1e-2,
@@ -271,16 +283,18 @@ class Engine:
         tf.train.Saver checkpoint, tf_util.py:259-264) or from the .npz
         save_state writes.  save_state removes the other format's files, so
         both exist only when another tool wrote one of them: then the newer
-        one is read, and equal modification times (a coarse filesystem clock)
-        are refused rather than resolved silently."""
+        one (nanosecond modification times) is read; on a tie (a copy that
+        kept timestamps, a tar archive's whole-second times) the TF1 bundle,
+        the reference's own format, is read and a warning names the choice."""
         from .common import tf_checkpoint as tfc
         path = self.checkpoint_path(fname)
         if tfc.is_bundle(fname) and os.path.isfile(path):
-            t_npz, t_tf1 = os.path.getmtime(path), os.path.getmtime(fname + ".index")
+            t_npz, t_tf1 = os.stat(path).st_mtime_ns, os.stat(fname + ".index").st_mtime_ns
             if t_npz == t_tf1:
-                raise ValueError(f"both {path} and the TF1 bundle {fname}.index exist with the same modification "
-                                 f"time; remove the one not to restore")
-            use_tf1 = t_tf1 > t_npz
+                import warnings
+                warnings.warn(f"both {path} and the TF1 bundle {fname}.index exist with the same modification "
+                              f"time; restoring the TF1 bundle (remove it to restore the .npz)")
+            use_tf1 = t_tf1 >= t_npz
         else:
             use_tf1 = tfc.is_bundle(fname)
         if use_tf1:
@@ -429,7 +443,7 @@ class Engine:
         rc = self._c("mdp_agent_update", int(agent), int(t), *[self._ptr(a) for a in args], out)
         self._keep = args
         self.sync_out()
-        return None if rc == 1 else list(out)
+        return None if rc == 1 else update_stats(out)
 
     def update_gate(self, t):
         return self._c("mdp_update_gate", int(t))

@@ -7,8 +7,11 @@ in one session shares one device engine (see ``common/tf_util.py``); its
 agent's buffer with that index (``:173-178``, fused into the grad kernels),
 target actors + target critic + fp64 TD target (``:180-187``), critic step
 (``:188``), actor step against the updated critic (``:191``), Polyak actor
-then critic (``:193-194``).  ``update`` returns the 6 stats of ``:196`` as a
-lazy sequence that synchronises only when read.
+then critic (``:193-194``).  ``update`` returns the 6 stats of ``:196`` as
+the reference does: a ``list`` of numpy scalars with its dtypes (``q_loss``,
+``p_loss`` and ``mean(target_q_next)`` fp32, the rest float64 --
+``engine.UPDATE_STAT_DTYPES``), read after the update (the reference's
+``session.run`` is synchronous too).
 
 ``model`` must be the reference's ``mlp_model`` (``train.py:39-46``: two
 hidden ReLU layers of ``args.num_units`` and a linear output, TF
@@ -23,6 +26,7 @@ import torch
 
 from .. import AgentTrainer
 from ..common import tf_util as U
+from ..engine import update_stats
 from .replay_buffer import ReplayBuffer
 
 
@@ -43,38 +47,6 @@ def check_model(model, num_units):
             "ReLU MLP (experiments/train.py:39-46) only")
     if not 1 <= int(num_units) <= MAX_UNITS:
         raise ValueError(f"--num-units {num_units}: the kernels take 1..{MAX_UNITS} hidden units")
-
-
-class UpdateStats(object):
-    """[q_loss, p_loss, mean(target_q), mean(rew), mean(target_q_next), std(target_q)]."""
-
-    def __init__(self, engine, agent):
-        self._host, self._event = engine.stats_future(agent)
-        self._vals = None
-
-    def _get(self):
-        if self._vals is None:
-            self._event.synchronize()
-            self._vals = [float(x) for x in self._host.tolist()]
-        return self._vals
-
-    def __getitem__(self, i):
-        return self._get()[i]
-
-    def __len__(self):
-        return 6
-
-    def __iter__(self):
-        return iter(self._get())
-
-    def __eq__(self, other):
-        return list(self._get()) == list(other)
-
-    def __repr__(self):
-        return repr(list(self._get()))
-
-    def tolist(self):
-        return list(self._get())
 
 
 class MADDPGAgentTrainer(AgentTrainer):
@@ -142,4 +114,6 @@ class MADDPGAgentTrainer(AgentTrainer):
         idx = self.replay_buffer.make_index_device(self.args.batch_size)   # :167
         self.replay_sample_index = idx
         eng.update(self.agent_index, idx=idx)                           # :173-194
-        return UpdateStats(eng, self.agent_index)
+        host, ev = eng.stats_future(self.agent_index)
+        ev.synchronize()
+        return update_stats(host.tolist())                              # :196

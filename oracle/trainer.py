@@ -115,6 +115,20 @@ def apply_grads(opt, params, g, grad_clip=0.5):
     opt.apply(params, {k: nets.clip_by_norm(v, grad_clip) for k, v in g.items()})
 
 
+def reference_stats(st, p_loss):
+    """``update()``'s return value (maddpg.py:196) with the reference's dtypes:
+    ``q_loss`` / ``p_loss`` are the fp32 scalars ``U.function`` fetches from
+    TF1 (``:91``, ``:54-56``; TF's fp32 ``reduce_mean`` accumulation order is
+    unpinned -- restated as the fp64 mean rounded once to fp32);
+    ``np.mean(target_q_next)`` is numpy's mean of the fp32 Q' array (fp32,
+    ``:185``); ``np.mean(target_q)``, ``np.mean(rew)`` and ``np.std(target_q)``
+    are float64 (the TD target is fp64, ``:186``; rewards come from the float64
+    replay arrays)."""
+    tq = st["target_q"]
+    return [np.float32(st["q_loss"]), np.float32(p_loss), np.float64(np.mean(tq)), np.float64(np.mean(st["rew"])),
+            np.mean(st["target_q_next"].astype(F32)), np.float64(np.std(tq))]
+
+
 def update_batch(agents, i, batch_n, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
     """``update`` on already-gathered batches batch_n[j] = sample_index(idx) of agent j."""
     ag = agents[i]
@@ -124,10 +138,7 @@ def update_batch(agents, i, batch_n, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
     apply_grads(ag.opt_actor, ag.actor, gp, grad_clip)
     nets.polyak(ag.tgt_actor, ag.actor)                            # :193
     nets.polyak(ag.tgt_critic, ag.critic)                          # :194
-    tq = st["target_q"]
-    return [st["q_loss"], p_loss, float(np.mean(tq)), float(np.mean(st["rew"])),
-            float(np.mean(st["target_q_next"].astype(np.float64))), float(np.std(tq))], \
-        {"grad_critic": gq, "grad_actor": gp}
+    return reference_stats(st, p_loss), {"grad_critic": gq, "grad_actor": gp}
 
 
 def update_round_throughput(agents, buffers, idx_n, u_tgt_n, u_act_n, gamma=0.95, grad_clip=0.5):
@@ -143,9 +154,7 @@ def update_round_throughput(agents, buffers, idx_n, u_tgt_n, u_act_n, gamma=0.95
         gq, st = critic_grads(agents, i, batch_n, u_tgt_n[i], gamma)
         gp, p_loss = actor_grads(agents, i, batch_n, u_act_n[i])
         grads.append((gq, gp))
-        tq = st["target_q"]
-        stats.append([st["q_loss"], p_loss, float(np.mean(tq)), float(np.mean(st["rew"])),
-                      float(np.mean(st["target_q_next"].astype(np.float64))), float(np.std(tq))])
+        stats.append(reference_stats(st, p_loss))
     for i, ag in enumerate(agents):
         gq, gp = grads[i]
         apply_grads(ag.opt_critic, ag.critic, gq, grad_clip)

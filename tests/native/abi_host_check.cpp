@@ -279,6 +279,117 @@ static bool all_finite(const double* v, int n) {
   return true;
 }
 
+// rc < 0 and the message names the refusal `why`: nothing was launched
+#define CHECK_REFUSED(h, call, why)                                               \
+  do {                                                                            \
+    const long long rc__ = (long long)(call);                                     \
+    ++g_checks;                                                                   \
+    if (rc__ >= 0 || std::strstr(mdp_last_error(h), why) == nullptr) {            \
+      ++g_fail;                                                                   \
+      std::fprintf(stderr, "FAIL %s:%d: %s -> %lld (%s)\n", __FILE__, __LINE__,   \
+                   #call, rc__, mdp_last_error(h));                               \
+    }                                                                             \
+  } while (0)
+
+static int lay_stride(mdp_handle* h) {
+  int32_t lay[6] = {};
+  return mdp_row_layout(h, 0, lay) == 0 ? lay[5] : 0;
+}
+
+// Every "_dev" argument of every entry point refuses host memory (malloc, the
+// stack, pinned hipHostMalloc) and a device buffer shorter than the call
+// needs, returning < 0 with a message before any launch -- a host address that
+// reached a kernel faulted the GPU in round 5 (r05h).  The handle
+// stays usable: the caller's lifecycle continues on it afterwards.
+static void host_pointers_refused(mdp_handle* h, const mdp_config& c, int32_t* idx, float* rows, float* obs,
+                                  float* act, float* q, float* u, float* info) {
+  const int n = c.n_agents, B = c.batch_size, E = c.num_envs;
+  const size_t big = (size_t)64 << 20;  // larger than any buffer a call here reads or writes
+  void* hb = std::malloc(big);
+  CHECK(hb != nullptr);
+  std::memset(hb, 0, big);
+  float* hf = (float*)hb;
+  int32_t* hi = (int32_t*)hb;
+  int64_t* hl = (int64_t*)hb;
+  const char* NDM = "not device memory";
+  CHECK_REFUSED(h, mdp_buffer_add_rows(h, hf, 4), NDM);
+  CHECK_REFUSED(h, mdp_buffer_put_agent(h, 0, hl, rows, 4), NDM);
+  CHECK_REFUSED(h, mdp_buffer_put_agent(h, 0, (int64_t*)idx, hf, 4), NDM);
+  CHECK_REFUSED(h, mdp_make_index(h, B, hi), NDM);
+  CHECK_REFUSED(h, mdp_sample_rows(h, hi, B, rows), NDM);
+  CHECK_REFUSED(h, mdp_sample_rows(h, idx, B, hf), NDM);
+  CHECK_REFUSED(h, mdp_act(h, 0, 0, hf, act, B, nullptr), NDM);
+  CHECK_REFUSED(h, mdp_act(h, 0, 0, obs, hf, B, nullptr), NDM);
+  CHECK_REFUSED(h, mdp_act(h, 0, 1, obs, act, B, hf), NDM);
+  CHECK_REFUSED(h, mdp_actor_logits(h, 0, 0, hf, act, B), NDM);
+  CHECK_REFUSED(h, mdp_actor_logits(h, 0, 0, obs, hf, B), NDM);
+  CHECK_REFUSED(h, mdp_q_values(h, 0, 0, hf, q, B), NDM);
+  CHECK_REFUSED(h, mdp_q_values(h, 0, 0, rows, hf, B), NDM);
+  CHECK_REFUSED(h, mdp_update(h, 0, hi, nullptr, nullptr), NDM);
+  CHECK_REFUSED(h, mdp_update(h, 0, idx, hf, nullptr), NDM);
+  CHECK_REFUSED(h, mdp_update(h, 0, idx, nullptr, hf), NDM);
+  double st6[6];
+  CHECK_REFUSED(h, mdp_agent_update(h, 0, 100, hi, u, st6), NDM);
+  CHECK_REFUSED(h, mdp_agent_update(h, 0, 100, idx, hf, st6), NDM);
+  CHECK_REFUSED(h, mdp_critic_grad(h, 0, hi, u), NDM);
+  CHECK_REFUSED(h, mdp_critic_grad(h, 0, idx, hf), NDM);
+  CHECK_REFUSED(h, mdp_actor_grad(h, 0, hi, u), NDM);
+  CHECK_REFUSED(h, mdp_actor_grad(h, 0, idx, hf), NDM);
+  CHECK_REFUSED(h, mdp_env_step(h, hf, nullptr), NDM);
+  CHECK_REFUSED(h, mdp_env_step(h, nullptr, hf), NDM);
+  CHECK_REFUSED(h, mdp_env_obs(h, hf), NDM);
+  CHECK_REFUSED(h, mdp_env_step_bench(h, hf), NDM);
+  // the stack and pinned host memory are host memory too
+  int32_t on_stack[16] = {};
+  CHECK_REFUSED(h, mdp_make_index(h, 16, on_stack), NDM);
+  void* pinned = nullptr;
+  HIP_OR_DIE(hipHostMalloc(&pinned, 4 * (size_t)B * 8, hipHostMallocDefault));
+  CHECK_REFUSED(h, mdp_act(h, 0, 0, obs, (float*)pinned, B, nullptr), NDM);
+  HIP_OR_DIE(hipHostFree(pinned));
+  // device buffers shorter than the call needs: the last 4 bytes the call
+  // would touch lie one float past the end of a 4 MiB allocation.  Run only
+  // where the runtime reports that allocation's exact extent (the library
+  // checks with the same hipMemGetAddressRange), so a runtime that rounds
+  // extents can never let a kernel read past a mapping here.
+  {
+    const size_t FB = (size_t)4 << 20, NF = FB / 4;
+    float* four = nullptr;
+    HIP_OR_DIE(hipMalloc((void**)&four, FB));
+    hipDeviceptr_t base = nullptr;
+    size_t ext = 0;
+    const bool exact = hipMemGetAddressRange(&base, &ext, (hipDeviceptr_t)four) == hipSuccess &&
+                       base == (hipDeviceptr_t)four && ext == FB;
+    std::printf("  short-buffer checks %s (extent %zu of %zu)\n", exact ? "on" : "skipped", ext, FB);
+    if (exact) {
+      const char* SHORT = "allocation too small";
+      const size_t stride = (size_t)lay_stride(h);
+      CHECK_REFUSED(h, mdp_make_index(h, B, (int32_t*)(four + NF - B + 1)), SHORT);
+      CHECK_REFUSED(h, mdp_sample_rows(h, idx, B, four + NF - (size_t)B * stride + 1), SHORT);
+      CHECK_REFUSED(h, mdp_q_values(h, 0, 0, rows, four + NF - B + 1, B), SHORT);
+      CHECK_REFUSED(h, mdp_env_step_bench(h, four + NF - (size_t)E * n * MDP_BENCH_W + 1), SHORT);
+      CHECK_REFUSED(h, mdp_update(h, 0, idx, four + NF - (size_t)n * B * 5 + 1, nullptr), SHORT);
+      // exactly long enough is accepted (the last float of the allocation)
+      CHECK_OK(h, mdp_q_values(h, 0, 0, rows, four + NF - B, B));
+    }
+    CHECK_OK(h, mdp_synchronize(h));
+    HIP_OR_DIE(hipFree(four));
+  }
+  // an arena in host memory: mdp_create fails, and the failed handle refuses everything
+  {
+    int64_t pt = 0;
+    const int64_t need = mdp_arena_bytes(&c, &pt);
+    if (need > 0 && (size_t)need <= big) {
+      mdp_handle* hh = nullptr;
+      CHECK(mdp_create(&c, hb, need, nullptr, &hh) < 0);
+      CHECK(hh != nullptr && std::strstr(mdp_last_error(hh), "arena_dev") != nullptr);
+      null_handle_entries(hh);
+      CHECK(mdp_destroy(hh) == 0);
+    }
+  }
+  std::free(hb);
+  CHECK_OK(h, mdp_synchronize(h));  // nothing faulted, nothing was launched
+}
+
 static void lifecycle(const mdp_config& c, const char* name) {
   std::printf("gpu lifecycle: %s\n", name);
   std::fflush(stdout);
@@ -386,6 +497,7 @@ static void lifecycle(const mdp_config& c, const char* name) {
     for (auto& x : hu) x = ((float)(lcg(seed) % 65535) + 1.f) / 65537.f;
     HIP_OR_DIE(hipMemcpy(u, hu.data(), 4 * hu.size(), hipMemcpyHostToDevice));
   }
+  host_pointers_refused(h, c, idx, rows, obs, act, q, u, info);
   CHECK_OK(h, mdp_make_index(h, n * B, idx));
   CHECK_ERR(h, mdp_make_index(h, -1, idx));
   CHECK_OK(h, mdp_sample_rows(h, idx, B, rows));

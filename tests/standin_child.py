@@ -131,10 +131,30 @@ def throughput():
     loss, par = oracle_err(a, agents, want)
     sp = spans(a)
     last = max(o + n for o, n in sp.values())
-    return dict(allreduces=len(log), recv_is_grad_base=all(x["recv"] == grad.data_ptr() for x in log),
-                count=[x["count"] for x in log], covers_every_net=bool(log) and log[0]["count"] >= last,
-                nranks=sorted({x["nranks"] for x in log}), dp_vs_single_max_diff=max_param_diff(a, b),
-                loss_rel_err=loss, param_abs_err=par)
+    out = dict(allreduces=len(log), recv_is_grad_base=all(x["recv"] == grad.data_ptr() for x in log),
+               count=[x["count"] for x in log], covers_every_net=bool(log) and log[0]["count"] >= last,
+               nranks=sorted({x["nranks"] for x in log}), dp_vs_single_max_diff=max_param_diff(a, b),
+               loss_rel_err=loss, param_abs_err=par)
+    # two more rounds, the device noise and index stream this time: the update
+    # counter (Ctl.upd_ctr, the Philox counter of the actor-loss samples) must
+    # advance by n per round on the data-parallel path as on one GPU -- the
+    # general kernels' pair lists bump it once, in the step pass
+    for _ in range(2):
+        a.update_all()
+        b.update_all()
+    a.synchronize()
+    b.synchronize()
+    calls()
+    out.update(rounds=3, n=a.n, upd_ctr=[upd_ctr(a), upd_ctr(b)], dp_vs_single_after=max_param_diff(a, b))
+    return out
+
+
+CTL_UPD_CTR_OFFSET = 2568  # Ctl.upd_ctr (mdp_topo.h; tests/test_gpu_parity.py)
+
+
+def upd_ctr(eng):
+    ctl = eng.region("ctl", torch.uint8).cpu().numpy()
+    return int(ctl[CTL_UPD_CTR_OFFSET:CTL_UPD_CTR_OFFSET + 4].view(np.uint32)[0])
 
 
 def graph():

@@ -26,11 +26,13 @@ def test_plan_single_gpu_runs_in_process():
 
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_plan_without_world_size_launches_n_ranks(n):
-    plan = bench.rank_launch_plan(n, {}, ["--gpus", str(n), "--steps", "7"], port=29555)
+    plan = bench.rank_launch_plan(n, {}, ["--gpus", str(n), "--steps", "7"])
     assert plan[:3] == [sys.executable, "-m", "torch.distributed.run"]
     assert f"--nproc-per-node={n}" in plan and "--nnodes=1" in plan
-    assert plan[plan.index("--master-addr") + 1] == "127.0.0.1"
-    assert plan[plan.index("--master-port") + 1] == "29555"
+    # torchrun's rendezvous store picks its own port (no probe-then-bind race)
+    assert "--rdzv-backend=c10d" in plan and "--rdzv-endpoint=127.0.0.1:0" in plan
+    assert plan[plan.index("--local-addr") + 1] == "127.0.0.1"
+    assert "--rdzv-endpoint=127.0.0.1:29555" in bench.rank_launch_plan(n, {}, [], port=29555)
     assert plan[-4:] == ["--gpus", str(n), "--steps", "7"]
     assert os.path.basename(plan[-5]) == "bench.py"
 

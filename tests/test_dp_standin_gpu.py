@@ -70,6 +70,10 @@ def test_standin_throughput_one_allreduce_per_round_vs_oracle(G, general):
     assert out["dp_vs_single_max_diff"] == 0.0
     assert out["loss_rel_err"] <= 1e-5
     assert out["param_abs_err"] < 2e-4
+    # k rounds advance the update counter by n k on both paths (the
+    # general kernels' pair lists bump it once per round, in the step pass)
+    assert out["upd_ctr"] == [out["n"] * out["rounds"]] * 2
+    assert out["dp_vs_single_after"] == 0.0
 
 
 @pytest.mark.parametrize("graphs,G", [("0", 2), ("1", 2), ("1", 8)])

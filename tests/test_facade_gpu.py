@@ -100,7 +100,14 @@ def test_trainer_facade_in_reference_loop(tmp_path):
                 trained += 1
                 want = ref_rng.make_index(len(ag.replay_buffer), 64)
                 np.testing.assert_array_equal(ag.replay_sample_index.cpu().numpy(), want)
-                assert len(loss) == 6 and all(np.isfinite(list(loss)))
+                # the reference's return value (maddpg.py:196): a list; q_loss, p_loss
+                # and mean(target_q_next) fp32 (TF1 fetches / an fp32 array's mean),
+                # mean / std of the fp64 TD target and mean(rew) float64
+                assert type(loss) is list and len(loss) == 6 and all(np.isfinite(loss))
+                assert [type(x) for x in loss] == [np.float32, np.float32, np.float64, np.float64,
+                                                   np.float32, np.float64]
+                dev = U.get_session().engine().stats(ag.agent_index)      # the fp64 device stats
+                assert [float(x) for x in loss] == [float(t(v)) for t, v in zip(map(type, loss), dev)]
         assert trained == 3 * 2            # gate opens at 320 rows: t = 400, 500
         assert random.getstate()[1] == ref_rng.state()
         # p_debug / q_debug surfaces

@@ -18,7 +18,7 @@ torch = pytest.importorskip("torch")
 if not torch.cuda.is_available():
     pytest.skip("no ROCm GPU", allow_module_level=True)
 
-from maddpg_amd.engine import Engine  # noqa: E402
+from maddpg_amd.engine import UPDATE_STAT_DTYPES, Engine  # noqa: E402
 from oracle import mpe, nets, trainer  # noqa: E402
 from tests.helpers import (case_names, golden_case, joint_rows, relu_margin_clean_idx, row_layout,  # noqa: E402
                            synthetic_trainer_case)
@@ -532,14 +532,19 @@ def test_torch_distributed_throughput_round_parity():
                 assert np.max(np.abs(got[k] - ref[k].reshape(got[k].shape))) < 2e-4, (i, w, k)
 
 
-@pytest.mark.parametrize("cfg", ["spread", "tag6_h128"])
+@pytest.mark.parametrize("cfg", ["spread", "tag6_h128", "tag_ddpg_h64"])
 def test_throughput_mode_train_step_graph_equals_eager(cfg):
     """mdp_train_step in throughput mode (rollout + k rounds as one graph) is the
     same work as env_step + k x update_round in throughput mode (tag6_h128: the
-    general kernels, one gradient launch per agent and step kind)."""
+    general kernels, one gradient launch per agent and step kind; tag_ddpg_h64:
+    DDPG adversaries pass the register kernels' limits, the MADDPG good agent
+    (critic input 82) does not -- agent 0 alone would allow the critic-launch
+    prefetch, so every round after a step's first must still draw fresh
+    indices, in the optimizer pair launches)."""
     from maddpg_amd.runner import VecRunner
-    kw = (dict(n_agents=6, scenario_adversaries=4, num_units=128) if cfg == "tag6_h128" else {})
-    scen = "simple_tag" if cfg == "tag6_h128" else "simple_spread"
+    kw = {"tag6_h128": dict(n_agents=6, scenario_adversaries=4, num_units=128),
+          "tag_ddpg_h64": dict(num_adversaries=3, adv_policy="ddpg")}.get(cfg, {})
+    scen = "simple_spread" if cfg == "spread" else "simple_tag"
 
     def make():
         r = VecRunner(scen, 64, batch_size=128, capacity=20000, seed=3, train_every=16, **kw)
@@ -961,7 +966,10 @@ def test_agent_update_literal_abi_vs_oracle():
         u = np.concatenate([c["u_tgt"][i].ravel(), c["u_act"][i].ravel()])
         got = eng2.agent_update(i, 200, idx=torch.from_numpy(c["idx"][i]), u=torch.from_numpy(u))
         want, _ = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i])
-        assert got is not None and len(got) == 6
-        assert got == eng2.stats(i)
+        assert type(got) is list and len(got) == 6
+        # the reference's dtypes (maddpg.py:91,54-56,185,196), the oracle's too
+        assert [type(x) for x in got] == [type(x) for x in want] == list(UPDATE_STAT_DTYPES)
+        assert [float(x) for x in got] == [float(t(v)) for t, v in zip(UPDATE_STAT_DTYPES, eng2.stats(i))]
         assert abs(got[0] - want[0]) <= 1e-5 * abs(want[0]) + 1e-7, (got, want)
-        np.testing.assert_allclose(got[1:], want[1:], rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(np.array(got[1:], np.float64), np.array(want[1:], np.float64),
+                                   rtol=2e-5, atol=2e-6)

@@ -305,3 +305,18 @@ def test_bench_algorithmic_model_matches_survey():
     assert abs(bench.flops_critic_grad(s5, 0) / 1e6 - 2009) < 2
     assert abs(bench.bytes_critic_grad(s5, 0) / 1e6 - 6.40) < 0.01
     assert bench.MARKER_KINDS == ("allreduce", "gather")
+
+
+def test_update_stats_reference_dtypes():
+    """update()'s return value (maddpg.py:196) from the fp64 device stats: a
+    list; q_loss, p_loss (TF1 fp32 fetches, :91 / :54-56) and mean(Q') (the mean
+    of an fp32 array, :185) fp32; mean / std of the fp64 TD target and the mean
+    reward (:186) float64 -- each the device value rounded once."""
+    import numpy as np
+    from maddpg_amd.engine import update_stats
+    dev = [0.1234567891234, -1.5e-3, 3.000000001, -0.25, 7.123456789, 0.0625]
+    got = update_stats(dev)
+    assert type(got) is list
+    assert [type(x) for x in got] == [np.float32, np.float32, np.float64, np.float64, np.float32, np.float64]
+    assert [float(x) for x in got] == [float(np.float32(dev[0])), float(np.float32(dev[1])), dev[2], dev[3],
+                                       float(np.float32(dev[4])), dev[5]]

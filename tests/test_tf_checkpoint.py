@@ -157,7 +157,7 @@ class _FakeEngine:
         self.loaded = sd
 
 
-def test_load_state_picks_newer_format_and_refuses_a_tie(tmp_path):
+def test_load_state_picks_newer_format_and_breaks_a_tie(tmp_path):
     import os
 
     from maddpg_amd.engine import Engine
@@ -176,9 +176,15 @@ def test_load_state_picks_newer_format_and_refuses_a_tie(tmp_path):
     os.utime(npz, (500, 500))
     assert Engine.load_state(e, prefix) == prefix
     np.testing.assert_array_equal(e.loaded["agent_0/actor/W1"], sd["agent_0/actor/W1"])
+    # a tie (timestamps kept by a copy / a tar archive): the TF1 bundle, with a warning
     os.utime(npz, (1000, 1000))
-    with pytest.raises(ValueError, match="same modification time"):
-        Engine.load_state(e, prefix)
+    e.loaded = None
+    with pytest.warns(UserWarning, match="same modification time"):
+        assert Engine.load_state(e, prefix) == prefix
+    np.testing.assert_array_equal(e.loaded["agent_0/actor/W1"], sd["agent_0/actor/W1"])
+    # nanosecond resolution decides what whole seconds cannot
+    os.utime(npz, ns=(1000 * 10**9 + 1, 1000 * 10**9 + 1))
+    assert Engine.load_state(e, prefix) == npz
 
 
 def test_injected_tensor_sizes_are_checked():
