@@ -63,7 +63,7 @@ def max_param_diff(a, b):
 
 
 def oracle_err(eng, agents, want):
-    loss = max(abs(eng.stats(i)[0] - want[i][0]) / (abs(want[i][0]) + 1e-12) for i in range(eng.n))
+    loss = max(float(abs(eng.stats(i)[0] - want[i][0]) / (abs(want[i][0]) + 1e-12)) for i in range(eng.n))
     par = 0.0
     for i in range(eng.n):
         for w, ref in (("actor", agents[i].actor), ("critic", agents[i].critic),
