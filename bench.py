@@ -295,6 +295,46 @@ def configs2_per_gpu(args, steps=12, warmup=3):
     return out
 
 
+# What an N-GPU line of BASELINE configs[2] (simple_spread N=3, E = 4096 env
+# copies per rank, B = 1024, H = 64) should show before any 8-GPU node ran it
+# (DESIGN §5 "Expected 1 -> 8 GPU curve").  Each rank runs the single-GPU step
+# (measured on one MI355X, profiles/r05u_configs/s3_spread_e4096.json: 3.5602 ms
+# per step strict, 1.4274 ms throughput mode, 40.96 rounds per step, the
+# rollout 26 us) plus, per round, the gradient exchanges inside the optimizer
+# launches: 2N = 6 (strict) or 1 (throughput) at `exchange_us` each (every
+# chunk's store to the 7 peers and the wait for theirs: peer skew + the fabric).
+SCALE_MODEL = {"rollout_us": 26.0, "rounds_per_step": 40.96, "envs_per_rank": 4096, "n_agents": 3,
+               "step_us": {"strict": 3560.2, "throughput": 1427.4},
+               "exchanges_per_round": {"strict": 6, "throughput": 1},
+               # per-exchange cost: the one-GPU 2-rank rehearsal's 1.48 us (no fabric) as the
+               # floor, 3 us the central guess (+ an xGMI hop and peer skew), 5 us pessimistic
+               "exchange_us": {"low": 1.5, "mid": 3.0, "high": 5.0}}
+
+
+def predict_scaling(world, mode="strict", exchange_us=None):
+    """predicted env-steps/s, updates/s and weak-scaling efficiency of a
+    `world`-rank configs[2] line (SCALE_MODEL); exchange_us: None = the central
+    guess, or a measured per-exchange cost (the line's exchange_per_rank)"""
+    m = SCALE_MODEL
+    c = m["exchange_us"]["mid"] if exchange_us is None else float(exchange_us)
+    r1 = (m["step_us"][mode] - m["rollout_us"]) / m["rounds_per_step"]       # one round on one GPU
+    rn = r1 + (m["exchanges_per_round"][mode] * c if world > 1 else 0.0)
+    step = m["rollout_us"] + m["rounds_per_step"] * rn
+    env = world * m["envs_per_rank"] / step * 1e6
+    return {"env_steps_per_sec": round(env, 1),
+            "trainer_updates_per_sec": round(m["rounds_per_step"] * m["n_agents"] / step * 1e6, 1),
+            "round_us": round(rn, 2), "weak_scaling_efficiency": round(r1 / rn if world > 1 else 1.0, 4),
+            "exchange_us": c if world > 1 else 0.0}
+
+
+def exchange_limit_us(mode="strict", efficiency=0.8):
+    """the per-exchange cost above which the exchange, not the kernels, holds
+    the weak-scaling efficiency below `efficiency`"""
+    m = SCALE_MODEL
+    r1 = (m["step_us"][mode] - m["rollout_us"]) / m["rounds_per_step"]
+    return round(r1 * (1.0 / efficiency - 1.0) / m["exchanges_per_round"][mode], 2)
+
+
 def rank_launch_plan(gpus, environ, argv, port=None):
     """How `bench.py --gpus N` becomes N ranks (pure host logic, tested on CPU).
 
@@ -529,6 +569,22 @@ def main():
         exall = [None] * world
         dist.all_gather_object(exall, ex)
         dp_check["exchange_per_rank"] = exall
+    prediction = None
+    if (world > 1 and args.scenario == "simple_spread" and r.n == 3 and args.num_envs == 4096
+            and args.batch_size == 1024 and args.num_units == 64 and args.train_every == 100
+            and not args.rollout_only):
+        # the curve stated before the first 8-GPU run, and the same model
+        # with this run's own measured exchange cost plugged in
+        meas = [e.get("per_exchange_us") for e in dp_check.get("exchange_per_rank", []) if e]
+        meas = [x for x in meas if x is not None]
+        prediction = {"model": "per rank: the one-GPU configs[2] step + exchanges per round x per-exchange "
+                               "cost (bench.SCALE_MODEL, DESIGN §5)",
+                      "central": predict_scaling(world, args.update_mode),
+                      "range": [predict_scaling(world, args.update_mode, SCALE_MODEL["exchange_us"][k])
+                                ["env_steps_per_sec"] for k in ("high", "low")],
+                      "exchange_limits_scaling_above_us": exchange_limit_us(args.update_mode),
+                      "with_measured_exchange": (predict_scaling(world, args.update_mode, max(meas))
+                                                 if meas else None)}
     # the dominant kernel among those with a roofline model (the gradient launch
     # pair: MFMA; rollout, optimizer step: HBM)
     if per_kind["critic_grad"][1] and per_kind["critic_grad"][1] == per_kind["actor_grad"][1]:
@@ -687,6 +743,9 @@ def main():
             "roofline": roof,
             "throughput_mode": tp_fig,
         }
+        if prediction is not None:
+            out["predicted_value"] = prediction["central"]["env_steps_per_sec"]
+            out["prediction"] = prediction
         if (world == 1 and not args.no_configs2 and
                 not (args.scenario == "simple_spread" and r.n == 3 and args.num_envs == 4096)):
             out["configs2_per_gpu"] = configs2_per_gpu(args)

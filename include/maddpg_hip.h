@@ -13,11 +13,19 @@
  *
  * Conventions
  *  - All compute state lives in ONE device arena the caller allocates (a
- *    PyTorch uint8 CUDA tensor in practice) of mdp_arena_bytes() bytes; the
- *    library never allocates device memory itself.
+ *    PyTorch uint8 CUDA tensor in practice) of mdp_arena_bytes() bytes.  The
+ *    library's one device allocation of its own is the direct xGMI exchange
+ *    buffer (mdp_dp_xgmi_open: hipExtMallocWithFlags, uncached, IPC-exported,
+ *    [2 slots][world][params + probe] 64-bit words; freed by
+ *    mdp_dp_xgmi_close / mdp_destroy).
  *  - "_dev" pointers are device pointers on the handle's device; "_host"
  *    pointers are host memory.  Device-pointer calls are asynchronous on the
- *    handle's stream unless stated; host-pointer calls synchronise.
+ *    handle's stream unless stated; host-pointer calls synchronise.  Every
+ *    non-NULL "_dev" argument (and mdp_create's arena) is checked at entry
+ *    with hipPointerGetAttributes / hipMemGetAddressRange: host memory
+ *    (malloc, the stack, pinned hipHostMalloc), another device's memory or an
+ *    allocation shorter than the call reads or writes returns < 0 with a
+ *    message, before anything is launched.
  *  - Return 0 on success, 1 for "skipped" (update gates), <0 on error; the
  *    message is in mdp_last_error(h).  No C++ exception crosses the ABI.
  *  - One handle per GPU process; calls on one handle are not thread-safe.

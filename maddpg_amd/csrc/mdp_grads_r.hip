@@ -41,9 +41,110 @@
 // row tiles per workgroup for the grid: 16 rows (MDP_R)
 #define MDP_RW MDP_R
 
+// diagnostic build (make budget; tools/grad_budget.py): the phase points of
+// EVERY workgroup of agent MDP_BUDGET_AGENT's critic (kind 0) and actor (kind 1)
+// launches -- lane 0 of the wave that reaches a point stamps it into
+// g_bud[kind][wg][pt]: the MDP_STAMP / MDP_STAMPW points below, 62 the
+// workgroup's start (wave 0), 63 its end (the last wave), 28..32 the critic
+// step's CRIT_T points and 33..38 critic_pre's CPRE_T points (the latest wave)
+#ifdef MDP_BUDGET
+#ifndef MDP_BUDGET_AGENT
+#define MDP_BUDGET_AGENT 1
+#endif
+// The points are kept in LDS during the launch (a global store mid-kernel would
+// count in vmcnt and delay the kernel's own later load waits until its ack) and
+// written out by the workgroup's last wave at its end.  A point is one s_memtime
+// (the shader clock, ~40 cycles) with its lgkmcnt(0) and one LDS store from lane
+// 0; the workgroup's start and end also read s_memrealtime (100 MHz, one clock
+// for the GPU: slots 64, 65), which places it in the launch and calibrates the
+// shader clock.
+#define MDP_BUD_N 72
+__device__ unsigned long long g_bud[2][160][MDP_BUD_N];
+__shared__ int s_bud;  // this launch records into g_bud[s_bud] (-1: not the chosen agent's launch)
+__shared__ unsigned long long s_bud_t[MDP_BUD_N];
+__shared__ unsigned s_bud_cnt;
+// MDP_BUDGET_REP = 2: every point stamped twice (the first value kept), so the
+// stamps' own cost can be extrapolated away (tools/grad_budget.py: t0 = 2 t1 - t2)
+#ifndef MDP_BUDGET_REP
+#define MDP_BUDGET_REP 1
+#endif
+// (the builtin, not an asm statement with a memory clobber: that clobber is a
+// compiler barrier at every point and cost the launch ~1.4 us of lost load /
+// LDS overlap, measured -- r06f; the builtin leaves the schedule to the
+// compiler, which places the stamp's wait at its LDS store)
+__device__ __forceinline__ unsigned long long bud_now() {
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+#if MDP_BUDGET_REP > 1
+  const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+  asm volatile("" ::"s"(t2));
+#endif
+  return t;
+}
+__device__ __forceinline__ unsigned long long bud_real() { return __builtin_amdgcn_s_memrealtime(); }
+#define BUD(i)                                           \
+  do {                                                   \
+    const unsigned long long t__ = bud_now();            \
+    if ((threadIdx.x & 63) == 0) s_bud_t[i] = t__;       \
+  } while (0)
+#define BUDMAX(i)                                        \
+  do {                                                   \
+    const unsigned long long t__ = bud_now();            \
+    if ((threadIdx.x & 63) == 0) atomicMax(&s_bud_t[i], t__); \
+  } while (0)
+// wave 0 clears the points and stamps the start before anything else
+#define BUD_BEGIN(k, agent_, multi_)                                          \
+  do {                                                                        \
+    s_bud = ((agent_) == MDP_BUDGET_AGENT && (multi_) <= 1) ? (k) : -1;       \
+    if (threadIdx.x < 64) {                                                   \
+      s_bud_t[threadIdx.x] = 0ull;                                            \
+      if (threadIdx.x < MDP_BUD_N - 64) s_bud_t[64 + threadIdx.x] = 0ull;     \
+      if (threadIdx.x == 0) s_bud_cnt = 0u;                                   \
+      const unsigned long long r__ = bud_real();                              \
+      if (threadIdx.x == 0) s_bud_t[64] = r__;                                \
+      BUD(62);                                                                \
+    }                                                                         \
+  } while (0)
+// every wave at its end; the last one writes the workgroup's points out
+#define MDP_WG_END(k)                                                                     \
+  do {                                                                                    \
+    BUDMAX(63);                                                                           \
+    {                                                                                     \
+      const unsigned long long r__ = bud_real();                                          \
+      if ((threadIdx.x & 63) == 0) atomicMax(&s_bud_t[65], r__);                          \
+    }                                                                                     \
+    unsigned c__ = 0u;                                                                    \
+    if ((threadIdx.x & 63) == 0) c__ = atomicAdd(&s_bud_cnt, 1u);                         \
+    c__ = __builtin_amdgcn_readfirstlane(c__);                                            \
+    if (c__ + 1u == (blockDim.x >> 6) && s_bud >= 0 && blockIdx.x < 160) {                \
+      const int l__ = threadIdx.x & 63;                                                   \
+      g_bud[s_bud][blockIdx.x][l__] = s_bud_t[l__];                                       \
+      if (l__ < MDP_BUD_N - 64) g_bud[s_bud][blockIdx.x][64 + l__] = s_bud_t[64 + l__];   \
+    }                                                                                     \
+  } while (0)
+#undef MDP_STAMP
+#undef MDP_STAMPW
+#define MDP_WG_START(k) \
+  do {                  \
+  } while (0)
+#ifdef MDP_BUDGET_MIN  // only the workgroups' start and end (what the points themselves cost)
+#define MDP_STAMP(i) (void)0
+#define MDP_STAMPW(i) (void)0
+#define CRIT_T(i) (void)0
+#define CPRE_T(i) (void)0
+#else
+#define MDP_STAMP(i) BUD(i)
+#define MDP_STAMPW(i) BUD(i)
+#define CRIT_T(i) BUDMAX(28 + (i))
+#define CPRE_T(i) BUDMAX(33 + (i))
+#endif
+#else
+#define BUD_BEGIN(k, agent_, multi_) (void)0
+#endif
+
 // diagnostic build: every workgroup's start (wave 0) and per-wave end of the
 // last critic (k = 0) / actor (k = 1) launch -- which role ends the launch
-#ifdef MDP_STAMPS
+#if defined(MDP_BUDGET)
+#elif defined(MDP_STAMPS)
 __device__ unsigned long long g_wg_t0[2][512];
 __device__ unsigned long long g_wg_t1[2][512][8];
 // critic_pre's per-wave phase points (row tile < 64, wave, point)
@@ -429,6 +530,7 @@ __device__ __forceinline__ void critic_pre_tile(const ActorArgs& a, float* lds, 
 
 __global__ __launch_bounds__(512) void k_critic_grad_r(CriticArgs a) {
   MDP_KARG_TOUCH("s"(a.agent), "s"(a.inv_b), "s"(a.pf_count), "s"(a.cpre_prev), "s"(a.topo.n), "s"(gridDim.x));
+  BUD_BEGIN(0, a.agent, a.multi);
   MDP_WG_START(0);
   MDP_TL(a.ctl, 0, 0);
   if (a.pf_count > 0 && blockIdx.x == gridDim.x - 1) {
@@ -891,6 +993,7 @@ __global__ __launch_bounds__(512) void k_actor_grad_r(ActorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_ready;
   __shared__ int fwd_issued;  // waves 0..3 issued the loads the critic forward needs first
+  BUD_BEGIN(1, a.agent, a.multi);
   MDP_WG_START(1);
   MDP_TL(a.ctl, 2, 0);
   int agent = a.agent, bx = blockIdx.x;
@@ -1172,6 +1275,18 @@ extern "C" int mdp_debug_tl_r(unsigned long long* out, int reset) {
 }
 #endif
 
+#ifdef MDP_BUDGET
+// [2][160][MDP_BUD_N] phase points of the chosen agent's last critic / actor launch; reset: zero them
+extern "C" int mdp_debug_budget(unsigned long long* out, int reset) {
+  const size_t n = sizeof(unsigned long long) * 2 * 160 * MDP_BUD_N;
+  if (reset) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_bud)) != hipSuccess) return -1;
+    return hipMemset(p, 0, n) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bud), n) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef MDP_STAMPS
 // diagnostic build: stamps of this translation unit's kernels (own code object)
 extern "C" int mdp_debug_stamps_r(unsigned long long* out, int n) {

@@ -68,3 +68,24 @@ def test_world_size_disagreeing_with_gpus_fails():
     r = _run(["--gpus", "8", "--launch-check"], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     assert r.returncode == 2
     assert "refusing" in r.stderr and not r.stdout.strip()
+
+
+def test_scaling_prediction_model():
+    """DESIGN §5's expected 1 -> 8 GPU curve (bench.predict_scaling): N = 1
+    reproduces the measured one-GPU configs[2] figure, every N > 1 rank pays its
+    exchanges per round, more exchange cost never predicts more, and the stated
+    limit is where the efficiency crosses 80 %."""
+    for mode, one in (("strict", 1150497.68), ("throughput", 2869503.58)):   # profiles/r05u_configs/s3
+        p1 = bench.predict_scaling(1, mode)
+        assert abs(p1["env_steps_per_sec"] / one - 1) < 1e-3 and p1["weak_scaling_efficiency"] == 1.0
+        prev = None
+        for n in (2, 4, 8):
+            lo, mid, hi = (bench.predict_scaling(n, mode, bench.SCALE_MODEL["exchange_us"][k])
+                           for k in ("low", "mid", "high"))
+            assert lo["env_steps_per_sec"] > mid["env_steps_per_sec"] > hi["env_steps_per_sec"]
+            assert mid["env_steps_per_sec"] < n * p1["env_steps_per_sec"]
+            if prev:
+                assert abs(mid["env_steps_per_sec"] / prev - n / (n // 2)) < 1e-6   # weak scaling past N = 2
+            prev = mid["env_steps_per_sec"]
+        lim = bench.exchange_limit_us(mode)
+        assert abs(bench.predict_scaling(8, mode, lim)["weak_scaling_efficiency"] - 0.8) < 1e-3
