@@ -405,8 +405,25 @@ int need_dev(mdp_handle* h, const void* p, int64_t bytes, const char* fn, const 
   // the next launch's hipGetLastError check would report it
   if (e != hipSuccess) (void)hipGetLastError();
   const bool managed = a.isManaged || a.type == hipMemoryTypeManaged;
-  if (e != hipSuccess || !(a.type == hipMemoryTypeDevice || managed))
+  if (e != hipSuccess || !(a.type == hipMemoryTypeDevice || managed)) {
+    // virtual-memory mappings (hipMemCreate + hipMemMap, e.g. PyTorch's
+    // expandable segments) the attributes may not know: the allocation handle
+    // names the device; the mapped range's extent is not checked.  Asked only
+    // for addresses the runtime does not know at all (pinned host memory,
+    // type Host, crashed hipMemRetainAllocationHandle in ROCm 7.2: r06k)
+    hipMemGenericAllocationHandle_t ah;
+    if ((e != hipSuccess || a.type == hipMemoryTypeUnregistered) &&
+        hipMemRetainAllocationHandle(&ah, const_cast<void*>(p)) == hipSuccess) {
+      hipMemAllocationProp prop;
+      std::memset(&prop, 0, sizeof(prop));
+      const bool ok = hipMemGetAllocationPropertiesFromHandle(&prop, ah) == hipSuccess &&
+                      prop.location.type == hipMemLocationTypeDevice && prop.location.id == h->device;
+      (void)hipMemRelease(ah);
+      if (ok) return 0;
+    }
+    (void)hipGetLastError();
     return refuse("is not device memory (a host address would fault the GPU); pass a buffer of the handle's device");
+  }
   if (!managed && a.device != h->device) return refuse("is memory of another device than the handle's");
   if (!managed && bytes > 0) {
     hipDeviceptr_t base = nullptr;
