@@ -404,23 +404,10 @@ int need_dev(mdp_handle* h, const void* p, int64_t bytes, const char* fn, const 
   // an unknown (host) address may set the runtime's last error: clear it, or
   // the next launch's hipGetLastError check would report it
   if (e != hipSuccess) (void)hipGetLastError();
+  // (device memory mapped with hipMemCreate + hipMemMap -- PyTorch's expandable
+  // segments -- reports type Device too: tests/native/abi_host_check.cpp, r06r)
   const bool managed = a.isManaged || a.type == hipMemoryTypeManaged;
   if (e != hipSuccess || !(a.type == hipMemoryTypeDevice || managed)) {
-    // virtual-memory mappings (hipMemCreate + hipMemMap, e.g. PyTorch's
-    // expandable segments) the attributes may not know: the allocation handle
-    // names the device; the mapped range's extent is not checked.  Asked only
-    // for addresses the runtime does not know at all (pinned host memory,
-    // type Host, crashed hipMemRetainAllocationHandle in ROCm 7.2: r06k)
-    hipMemGenericAllocationHandle_t ah;
-    if ((e != hipSuccess || a.type == hipMemoryTypeUnregistered) &&
-        hipMemRetainAllocationHandle(&ah, const_cast<void*>(p)) == hipSuccess) {
-      hipMemAllocationProp prop;
-      std::memset(&prop, 0, sizeof(prop));
-      const bool ok = hipMemGetAllocationPropertiesFromHandle(&prop, ah) == hipSuccess &&
-                      prop.location.type == hipMemLocationTypeDevice && prop.location.id == h->device;
-      (void)hipMemRelease(ah);
-      if (ok) return 0;
-    }
     (void)hipGetLastError();
     return refuse("is not device memory (a host address would fault the GPU); pass a buffer of the handle's device");
   }

@@ -374,6 +374,42 @@ static void host_pointers_refused(mdp_handle* h, const mdp_config& c, int32_t* i
     CHECK_OK(h, mdp_synchronize(h));
     HIP_OR_DIE(hipFree(four));
   }
+  // device memory mapped through the virtual-memory API (hipMemCreate +
+  // hipMemMap, what PyTorch's expandable segments use) is accepted
+  {
+    hipMemAllocationProp prop;
+    std::memset(&prop, 0, sizeof(prop));
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    size_t gran = 0;
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) == hipSuccess && gran) {
+      const size_t sz = ((4 * (size_t)n * B + gran - 1) / gran) * gran;
+      hipMemGenericAllocationHandle_t mh;
+      void* va = nullptr;
+      HIP_OR_DIE(hipMemCreate(&mh, sz, &prop, 0));
+      HIP_OR_DIE(hipMemAddressReserve(&va, sz, 0, nullptr, 0));
+      HIP_OR_DIE(hipMemMap(va, sz, 0, mh, 0));
+      hipMemAccessDesc acc;
+      acc.location = prop.location;
+      acc.flags = hipMemAccessFlagsProtReadWrite;
+      HIP_OR_DIE(hipMemSetAccess(va, sz, &acc, 1));
+      hipPointerAttribute_t pa;
+      std::memset(&pa, 0, sizeof(pa));
+      const hipError_t pe = hipPointerGetAttributes(&pa, va);
+      (void)hipGetLastError();
+      std::printf("  virtual-memory mapping: hipPointerGetAttributes %s, type %d\n", hipGetErrorString(pe), (int)pa.type);
+      CHECK_OK(h, mdp_make_index(h, n * B, (int32_t*)va));
+      CHECK_OK(h, mdp_sample_rows(h, (const int32_t*)va, B, rows));
+      CHECK_OK(h, mdp_synchronize(h));
+      HIP_OR_DIE(hipMemUnmap(va, sz));
+      HIP_OR_DIE(hipMemAddressFree(va, sz));
+      HIP_OR_DIE(hipMemRelease(mh));
+    } else {
+      (void)hipGetLastError();
+      std::printf("  virtual-memory mapping: not supported here, skipped\n");
+    }
+  }
   // an arena in host memory: mdp_create fails, and the failed handle refuses everything
   {
     int64_t pt = 0;
