@@ -246,6 +246,13 @@ def test_update_parity_spread_b1024():
     _update_parity([18, 18, 18], B=1024, L=4000, seed=21)
 
 
+@pytest.mark.parametrize("seed", [0, 1, 12345])
+def test_update_parity_spread_survey_seeds(seed):
+    # SURVEY 8d's synthetic-input seeds at BASELINE configs[1]'s update shape:
+    # simple_spread N=3, B=1024, the replay filled to the gate (L = B * 25)
+    _update_parity([18, 18, 18], B=1024, L=25600, seed=seed)
+
+
 def test_update_parity_simple():
     _update_parity([4], B=1024, L=2000, seed=22)
 
