@@ -52,8 +52,7 @@ def test_bench_two_ranks_driver_command_shape():
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(29400 + random.randrange(400)),
-           "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--num-envs", "256",
-           "--no-throughput-figure"]
+           "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-throughput-figure"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
@@ -63,3 +62,11 @@ def test_bench_two_ranks_driver_command_shape():
     dp = d["dp_check"]
     assert dp["replicas_identical"] is True
     assert dp["peers_per_rank"] == [1, 1]
+    # the default N > 1 workload (configs[2]: 4,096 env copies per rank) carries the
+    # expected curve of DESIGN §5 and the model with this run's exchange cost
+    assert d["config"]["num_envs_per_gpu"] == 4096
+    assert d["predicted_value"] == d["prediction"]["central"]["env_steps_per_sec"] > 0
+    lo, hi = sorted(d["prediction"]["range"])
+    assert lo < d["predicted_value"] < hi
+    assert d["prediction"]["exchange_limits_scaling_above_us"] > 0
+    assert d["prediction"]["with_measured_exchange"] is not None
