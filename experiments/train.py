@@ -68,6 +68,10 @@ def parse_args(argv=None):
     parser.add_argument("--save-format", choices=["npz", "tf1"], default="npz",
                         help="checkpoint format: npz, or tf1 (a tf.train.Saver checkpoint with the reference's "
                              "variable names; --load-dir reads either)")
+    parser.add_argument("--check-nan", action="store_true", default=False,
+                        help="debug: after every training step check every parameter, Adam slot and update stat "
+                             "for NaN / Inf and stop with 'Nan detected' (the reference's _Function(check_nan), "
+                             "tf_util.py:322,366-368)")
     parser.add_argument("--update-mode", choices=["strict", "throughput"], default="strict",
                         help="strict: the reference's update order; throughput: every agent's gradients from "
                              "the round-start parameters, then every optimizer step (SURVEY 8e, single GPU)")
@@ -227,8 +231,10 @@ def train(arglist):
     t_start = time.time()
     vec_steps = 0
     say('Starting iterations...')
+    from maddpg_amd.common.tf_util import check_nan
     while True:
-        runner.step()
+        if runner.step() and arglist.check_nan:
+            check_nan(runner.eng)
         vec_steps += 1
         if vec_steps % L:
             continue

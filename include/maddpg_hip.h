@@ -43,7 +43,7 @@ extern "C" {
 #define MDP_MAX_AGENTS 8
 #define MDP_ACT_DIM 5          /* MPE Discrete(dim_p*2+1) action spaces */
 #define MDP_MAX_UNITS 256      /* largest --num-units (train.py:24) */
-#define MDP_ABI_VERSION 4
+#define MDP_ABI_VERSION 5
 
 enum mdp_scenario {
     MDP_SCN_NONE = 0,          /* trainer only (no device env) */
@@ -261,6 +261,11 @@ int mdp_reduce_grad(mdp_handle* h, int32_t agent, int32_t net);
 int mdp_apply_grad(mdp_handle* h, int32_t agent, int32_t net, float scale);
 /* the 6 values update() returns (maddpg.py:196), fp64, synchronises */
 int mdp_get_stats(mdp_handle* h, int32_t agent, double out6[6]);
+/* debug check (the reference's _Function(check_nan), tf_util.py:322,366-368):
+ * *nonfinite_out = the number of NaN / Inf values in every parameter set
+ * (weights, targets, Adam m and v of every agent) and in the agents' update
+ * stats; counted on the device, synchronous (ABI 5) */
+int mdp_check_finite(mdp_handle* h, int64_t* nonfinite_out);
 
 /* ---- update mode of the round paths (mdp_update_round, mdp_train_step) ----
  * 0 strict (default): the reference's order -- agents in turn, each critic

@@ -22,7 +22,7 @@ MAX_AGENTS = 8
 ACT_DIM = 5
 BENCH_W = 8   # MDP_BENCH_W: floats per agent benchmark_data record
 MAX_UNITS = 256  # MDP_MAX_UNITS: largest --num-units
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 SCN = {"none": 0, "simple": 1, "simple_spread": 2, "simple_adversary": 3, "simple_tag": 4}
 WHICH = {"actor": 0, "critic": 1, "tgt_actor": 2, "tgt_critic": 3, "m_actor": 4, "v_actor": 5,
@@ -127,6 +127,7 @@ SIGNATURES = {
     "mdp_reduce_grad": (ctypes.c_int, [_P, _I32, _I32]),
     "mdp_apply_grad": (ctypes.c_int, [_P, _I32, _I32, ctypes.c_float]),
     "mdp_get_stats": (ctypes.c_int, [_P, _I32, _F64P]),
+    "mdp_check_finite": (ctypes.c_int, [_P, ctypes.POINTER(_I64)]),
     "mdp_env_reset": (ctypes.c_int, [_P]),
     "mdp_env_step": (ctypes.c_int, [_P, _P, _P]),
     "mdp_env_get_state": (ctypes.c_int, [_P, _F32P, _F32P, _I32P, _I32P]),

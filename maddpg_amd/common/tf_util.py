@@ -11,6 +11,7 @@ reference's update reads every agent's buffer with a shared index set
 (``maddpg.py:167-178``).
 """
 import contextlib
+import os
 import random
 
 import numpy as np
@@ -19,11 +20,14 @@ _DEFAULT = None
 
 
 class Session:
-    def __init__(self, seed=None):
+    def __init__(self, seed=None, check_nan=None):
         self.trainers = []
         self.buffers = []
         self._engine = None
         self.seed = seed
+        # the reference's _Function(check_nan) (tf_util.py:322,366-368; off there):
+        # when on, every update() checks the device state and raises "Nan detected"
+        self.check_nan = (os.environ.get("MDP_CHECK_NAN", "0") == "1") if check_nan is None else bool(check_nan)
 
     # trainers and their replay buffers register here
     def register(self, trainer):
@@ -85,19 +89,19 @@ def get_session():
     return _DEFAULT
 
 
-def make_session(num_cpu=1, seed=None):
+def make_session(num_cpu=1, seed=None, check_nan=None):
     """tf_util.make_session: num_cpu is accepted for signature parity (compute is on the GPU)."""
     global _DEFAULT
-    _DEFAULT = Session(seed=seed)
+    _DEFAULT = Session(seed=seed, check_nan=check_nan)
     return _DEFAULT
 
 
 @contextlib.contextmanager
-def single_threaded_session(seed=None):
+def single_threaded_session(seed=None, check_nan=None):
     """``with U.single_threaded_session():`` (experiments/train.py:79)."""
     global _DEFAULT
     prev = _DEFAULT
-    sess = make_session(1, seed)
+    sess = make_session(1, seed, check_nan)
     try:
         yield sess
     finally:
@@ -120,6 +124,13 @@ def load_state(fname, saver=None):
     """U.load_state (tf_util.py:259-264): a TF1 checkpoint at prefix fname
     (tf.train.Saver's files) or the .npz save_state writes."""
     return get_session().engine().load_state(fname)
+
+
+def check_nan(engine):
+    """tf_util.py:366-368 on the device state: raise RuntimeError("Nan detected")
+    when any parameter, target, Adam slot or update stat is NaN or Inf"""
+    if engine.check_finite():
+        raise RuntimeError("Nan detected")
 
 
 def sync_rng_to_device(engine):

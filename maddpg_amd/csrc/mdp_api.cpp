@@ -2395,6 +2395,29 @@ int mdp_env_obs(mdp_handle* h, float* obs_dev) {
   return 0;
 }
 
+// the reference's check_nan (tf_util.py:322,366-368, a debug option it never
+// enables): non-finite values in every parameter set (theta, target, Adam m
+// and v) and in every agent's 6 update stats, counted on the device;
+// synchronous, outside any graph
+int mdp_check_finite(mdp_handle* h, int64_t* nonfinite) {
+  MDP_NEED(h);
+  if (!nonfinite) return fail(h, "mdp_check_finite: nonfinite is null");
+  HIPCHK(h, hipMemsetAsync(&h->ctl->nonfinite, 0, sizeof(uint32_t), h->stream));
+  const float* sets[4] = {h->theta, h->target, h->m, h->v};
+  for (const float* p : sets) HIPCHK(h, mdp_launch_count_nonfinite(p, h->L.PT, &h->ctl->nonfinite, h->stream));
+  uint32_t c = 0;
+  const int n = h->cfg.n_agents;
+  std::vector<double> st(8 * (size_t)n);
+  HIPCHK(h, hipMemcpyAsync(&c, &h->ctl->nonfinite, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(st.data(), h->stats, sizeof(double) * st.size(), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  int64_t bad = c;
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < 6; ++k) bad += std::isfinite(st[8 * i + k]) ? 0 : 1;
+  *nonfinite = bad;
+  return 0;
+}
+
 int64_t mdp_episode_count(mdp_handle* h) {
   MDP_NEED(h);
   int64_t n = 0;

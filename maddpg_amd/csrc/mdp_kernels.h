@@ -398,6 +398,7 @@ hipError_t mdp_launch_polyak(float* target, const float* theta, int64_t n, float
                              hipStream_t s);
 hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx, int count, float* out,
                              hipStream_t s);
+hipError_t mdp_launch_count_nonfinite(const float* p, int64_t n, uint32_t* cnt, hipStream_t s);
 hipError_t mdp_launch_put_rows(float* replay, int stride, int64_t cap, int64_t next, const float* src, int64_t rows,
                                hipStream_t s);
 hipError_t mdp_launch_put_agent(float* replay, int stride, const ADesc& ag, const int64_t* pos, const float* cols,

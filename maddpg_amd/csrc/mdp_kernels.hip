@@ -64,6 +64,18 @@ __global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ r
 }
 
 // ring append of whole rows: replay[(next + r) % cap] = src[r]
+// ============================================================= check_nan
+// non-finite entries of a float span -- the reference's _Function(check_nan)
+// (tf_util.py:322,366-368) as an opt-in debug check (mdp_check_finite):
+// grid-stride; a thread that saw any adds its count with one integer atomic
+// (exact and order-independent; none at all on finite data)
+__global__ __launch_bounds__(256) void k_count_nonfinite(const float* __restrict__ p, int64_t n, uint32_t* cnt) {
+  uint32_t c = 0u;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += isfinite(p[i]) ? 0u : 1u;
+  if (c) atomicAdd(cnt, c);
+}
+
 __global__ __launch_bounds__(256) void k_put_rows(float* __restrict__ replay, int stride, int64_t cap,
                                                   int64_t next, const float* __restrict__ src, int64_t rows) {
   const int v4 = stride >> 2;
@@ -1163,6 +1175,14 @@ hipError_t mdp_launch_gather(const float* replay, int stride, const int32_t* idx
                        out + (int64_t)b0 * stride);
     MDP_CHECK_LAUNCH();
   }
+  return hipSuccess;
+}
+hipError_t mdp_launch_count_nonfinite(const float* p, int64_t n, uint32_t* cnt, hipStream_t s) {
+  int grid = (int)((n + 255) / 256);
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_count_nonfinite, dim3(grid), dim3(256), 0, s, p, n, cnt);
+  MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
 hipError_t mdp_launch_put_rows(float* replay, int stride, int64_t cap, int64_t next, const float* src, int64_t rows,

@@ -68,4 +68,6 @@ struct Ctl {
   uint64_t xw_ticks;    // summed over chunk exchanges
   uint64_t xw_count;    // chunk exchanges counted
   uint64_t xw_max;      // the longest single wait
+  uint32_t nonfinite;   // mdp_check_finite's count of non-finite parameters / Adam state
+  uint32_t pad2;
 };

@@ -606,6 +606,14 @@ class Engine:
         self._c("mdp_get_stats", agent, out)
         return list(out)
 
+    def check_finite(self):
+        """NaN / Inf values in every parameter set (weights, targets, Adam m, v)
+        and in the agents' update stats, counted on the device (mdp_check_finite:
+        the reference's opt-in check_nan, tf_util.py:322,366-368)"""
+        out = ctypes.c_int64()
+        self._c("mdp_check_finite", ctypes.byref(out))
+        return int(out.value)
+
     def stats_future(self, agent):
         """Snapshot of agent's 6 update stats, copied D2H in stream order (no sync);
         returns (host tensor, event) -- wait on the event before reading."""

@@ -116,4 +116,6 @@ class MADDPGAgentTrainer(AgentTrainer):
         eng.update(self.agent_index, idx=idx)                           # :173-194
         host, ev = eng.stats_future(self.agent_index)
         ev.synchronize()
+        if self.session.check_nan:                                      # tf_util.py:366-368
+            U.check_nan(eng)
         return update_stats(host.tolist())                              # :196

@@ -155,6 +155,7 @@ static void null_handle_entries(mdp_handle* h) {
   CHECK(mdp_reduce_grad(h, 0, 0) < 0);
   CHECK(mdp_apply_grad(h, 0, 0, 1.f) < 0);
   CHECK(mdp_get_stats(h, 0, d) < 0);
+  CHECK(mdp_check_finite(h, &off) < 0);
   CHECK(mdp_set_update_mode(h, 1) < 0);
   CHECK(mdp_update_all(h, nullptr, nullptr, nullptr) < 0);
   CHECK(mdp_env_reset(h) < 0);
@@ -515,6 +516,12 @@ static void lifecycle(const mdp_config& c, const char* name) {
   for (int i = 0; i < n; ++i) {
     CHECK_OK(h, mdp_get_stats(h, i, stats));
     CHECK(all_finite(stats, 6));
+  }
+  {
+    int64_t bad = -1;
+    CHECK_OK(h, mdp_check_finite(h, &bad));
+    CHECK(bad == 0);
+    CHECK_ERR(h, mdp_check_finite(h, nullptr));
   }
 
   // device buffers for the per-call paths

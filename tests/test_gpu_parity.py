@@ -980,3 +980,52 @@ def test_agent_update_literal_abi_vs_oracle():
         assert abs(got[0] - want[0]) <= 1e-5 * abs(want[0]) + 1e-7, (got, want)
         np.testing.assert_allclose(np.array(got[1:], np.float64), np.array(want[1:], np.float64),
                                    rtol=2e-5, atol=2e-6)
+
+
+def test_check_finite_counts_nan_and_inf():
+    """mdp_check_finite (the reference's opt-in check_nan, tf_util.py:322,366-368):
+    0 on a trained engine; a NaN weight and an Inf Adam slot are counted; the
+    facade raises the reference's "Nan detected" from update() when the session
+    asks for the check."""
+    dims, B, L = [18, 18, 18], 256, 1200
+    c = synthetic_trainer_case(dims, B, L, seed=51)
+    eng = Engine(dims, batch_size=B, capacity=L)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    eng.init_params(3)
+    eng.update(0, idx=torch.from_numpy(c["idx"][0]))
+    eng.synchronize()
+    assert eng.check_finite() == 0
+    w = eng.get_params(1, "critic")
+    w["W2"][3, 5] = np.nan
+    eng.set_params(1, "critic", w)
+    assert eng.check_finite() == 1
+    v = eng.get_params(2, "v_actor")
+    v["b1"][0] = np.inf
+    eng.set_params(2, "v_actor", v)
+    assert eng.check_finite() == 2
+
+
+def test_facade_check_nan_raises_like_the_reference():
+    import argparse
+
+    from maddpg_amd.common import tf_util as U
+    from maddpg_amd.envs import Discrete
+    from maddpg_amd.trainer.maddpg import MADDPGAgentTrainer
+    args = argparse.Namespace(lr=1e-2, gamma=0.95, batch_size=32, num_units=64, max_episode_len=2)
+    rng = np.random.default_rng(0)
+    with U.single_threaded_session(check_nan=True):
+        trainers = [MADDPGAgentTrainer(f"agent_{i}", None, [(18,)] * 3, [Discrete(5)] * 3, i, args)
+                    for i in range(3)]
+        U.initialize()
+        for _ in range(100):
+            obs = [rng.uniform(-1, 1, 18).astype(np.float32) for _ in range(3)]
+            act = [np.full(5, 0.2, np.float32) for _ in range(3)]
+            for i, ag in enumerate(trainers):
+                ag.experience(obs[i], act[i], -1.0, obs[i], False, False)
+        assert trainers[0].update(trainers, 100) is not None       # finite: trains, no raise
+        eng = U.get_session().engine()
+        w = eng.get_params(0, "actor")
+        w["W1"][0, 0] = np.nan
+        eng.set_params(0, "actor", w)
+        with pytest.raises(RuntimeError, match="Nan detected"):
+            trainers[1].update(trainers, 200)

@@ -15,7 +15,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     assert set(_lib.SIGNATURES) <= set(syms)
-    assert lib.mdp_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.mdp_abi_version() == _lib.ABI_VERSION == 5
 
 
 def _cfg(**kw):
