@@ -229,6 +229,7 @@ def train(arglist):
     E, L = arglist.num_envs, arglist.max_episode_len
     curve = LearningCurve(arglist.save_rate, arglist.num_episodes, n)
     t_start = time.time()
+    t_run = time.perf_counter()
     vec_steps = 0
     say('Starting iterations...')
     from maddpg_amd.common.tf_util import check_nan
@@ -263,6 +264,13 @@ def train(arglist):
             say('...Finished total of {} episodes.'.format(curve.length))
             break
     runner.synchronize()
+    # SURVEY 5's counters beside the reference's prints: env-steps/s (transitions
+    # of every env copy on every rank) and trainer-updates/s over the whole run
+    el = time.perf_counter() - t_run
+    runner.throughput = {"env_steps_per_sec": vec_steps * E * world / el,
+                         "trainer_updates_per_sec": runner.rounds * n / el, "seconds": el}
+    say('throughput: {:.1f} env-steps/s, {:.1f} trainer-updates/s over {:.2f} s'.format(
+        runner.throughput["env_steps_per_sec"], runner.throughput["trainer_updates_per_sec"], el))
     return runner
 
 

@@ -167,6 +167,9 @@ def test_train_cli_runs(tmp_path, capsys, scenario, extra):
     out = capsys.readouterr().out
     assert "Starting iterations..." in out and "...Finished total of" in out
     assert out.count("mean episode reward") >= 2
+    # SURVEY 5's throughput counters, after the reference's last line
+    assert out.rstrip().splitlines()[-1].startswith("throughput: ") and "env-steps/s" in out
+    assert runner.throughput["env_steps_per_sec"] > 0 and runner.throughput["trainer_updates_per_sec"] > 0
     assert os.path.exists(str(tmp_path) + "/t_rewards.pkl")
     assert runner.rounds > 0
     # restore the saved model into a fresh run
