@@ -68,6 +68,11 @@ def parse_args(argv=None):
     parser.add_argument("--save-format", choices=["npz", "tf1"], default="npz",
                         help="checkpoint format: npz, or tf1 (a tf.train.Saver checkpoint with the reference's "
                              "variable names; --load-dir reads either)")
+    # the reference's hard-coded constants, as flags with its values
+    parser.add_argument("--tau", type=float, default=1e-2, help="Polyak rate of the target nets (maddpg.py:21)")
+    parser.add_argument("--grad-clip", type=float, default=0.5, help="per-tensor clip_by_norm (maddpg.py:130,142)")
+    parser.add_argument("--actor-reg", type=float, default=1e-3, help="actor logits regulariser (maddpg.py:56)")
+    parser.add_argument("--buffer-size", type=int, default=int(1e6), help="replay capacity (maddpg.py:147)")
     parser.add_argument("--check-nan", action="store_true", default=False,
                         help="debug: after every training step check every parameter, Adam slot and update stat "
                              "for NaN / Inf and stop with 'Nan detected' (the reference's _Function(check_nan), "
@@ -207,6 +212,8 @@ def train(arglist):
                        num_units=arglist.num_units, lr=arglist.lr, gamma=arglist.gamma,
                        max_episode_len=arglist.max_episode_len, seed=arglist.seed,
                        train_every=arglist.train_every, world_size=world, rank=rank,
+                       tau=arglist.tau, grad_clip=arglist.grad_clip, actor_reg=arglist.actor_reg,
+                       capacity=arglist.buffer_size,
                        # the learning-curve windows of one terminal step span <= save_rate + E episodes
                        episode_log_rows=max(4096, 4 * arglist.num_envs, arglist.save_rate + 2 * arglist.num_envs))
     if arglist.update_mode != "strict":

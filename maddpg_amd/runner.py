@@ -44,7 +44,8 @@ class VecRunner:
     def __init__(self, scenario="simple_spread", num_envs=1024, *, n_agents=None, scenario_adversaries=None,
                  num_adversaries=0, good_policy="maddpg", adv_policy="maddpg", batch_size=1024,
                  num_units=64, lr=1e-2, gamma=0.95, max_episode_len=25, capacity=int(1e6), seed=0,
-                 train_every=100, world_size=1, rank=0, device=None, episode_log_rows=0):
+                 train_every=100, world_size=1, rank=0, device=None, episode_log_rows=0, tau=1e-2,
+                 grad_clip=0.5, actor_reg=1e-3):
         sp = envs.spec(scenario, n_agents, scenario_adversaries)
         self.spec = sp
         n = sp.n_agents
@@ -53,6 +54,7 @@ class VecRunner:
         self.eng = Engine(sp.obs_dims, local_q, num_units=num_units, batch_size=batch_size,
                           max_episode_len=max_episode_len, capacity=capacity, num_envs=num_envs,
                           scenario=scenario, num_adversaries=sp.num_adversaries, lr=lr, gamma=gamma,
+                          tau=tau, grad_clip=grad_clip, actor_reg=actor_reg,
                           seed=seed * 1000003 + 17, world_size=world_size, rank=rank, device=device,
                           episode_log_rows=episode_log_rows)
         self.eng.init_params(seed)                           # identical replicas on every rank

@@ -49,7 +49,7 @@ def act(ag, obs, u):
     return nets.gumbel_softmax(logits, u)
 
 
-def update(agents, i, buffers, idx, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
+def update(agents, i, buffers, idx, u_tgt, u_act, gamma=0.95, grad_clip=0.5, tau=1e-2, actor_reg=1e-3):
     """One ``agents[i].update(agents, t)`` past the gates (maddpg.py:167-196).
 
     buffers[j] = (obs[L,o_j], act[L,A], rew[L], obs_next[L,o_j], done[L]) of
@@ -57,7 +57,7 @@ def update(agents, i, buffers, idx, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
     """
     n = len(agents)
     batch_n = [tuple(x[idx] for x in buffers[j]) for j in range(n)]   # :173-178
-    return update_batch(agents, i, batch_n, u_tgt, u_act, gamma, grad_clip)
+    return update_batch(agents, i, batch_n, u_tgt, u_act, gamma, grad_clip, tau, actor_reg)
 
 
 def critic_grads(agents, i, batch_n, u_tgt, gamma=0.95):
@@ -129,15 +129,15 @@ def reference_stats(st, p_loss):
             np.mean(st["target_q_next"].astype(F32)), np.float64(np.std(tq))]
 
 
-def update_batch(agents, i, batch_n, u_tgt, u_act, gamma=0.95, grad_clip=0.5):
+def update_batch(agents, i, batch_n, u_tgt, u_act, gamma=0.95, grad_clip=0.5, tau=1e-2, actor_reg=1e-3):
     """``update`` on already-gathered batches batch_n[j] = sample_index(idx) of agent j."""
     ag = agents[i]
     gq, st = critic_grads(agents, i, batch_n, u_tgt, gamma)
     apply_grads(ag.opt_critic, ag.critic, gq, grad_clip)          # :188
-    gp, p_loss = actor_grads(agents, i, batch_n, u_act)            # :191 (post-step critic)
+    gp, p_loss = actor_grads(agents, i, batch_n, u_act, actor_reg)  # :191 (post-step critic)
     apply_grads(ag.opt_actor, ag.actor, gp, grad_clip)
-    nets.polyak(ag.tgt_actor, ag.actor)                            # :193
-    nets.polyak(ag.tgt_critic, ag.critic)                          # :194
+    nets.polyak(ag.tgt_actor, ag.actor, tau)                       # :193
+    nets.polyak(ag.tgt_critic, ag.critic, tau)                     # :194
     return reference_stats(st, p_loss), {"grad_critic": gq, "grad_actor": gp}
 
 

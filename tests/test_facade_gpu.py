@@ -157,6 +157,9 @@ def test_trainer_facade_in_reference_loop(tmp_path):
     ("simple_tag", ["--num-adversaries", "3"]),
     ("simple", []),
     ("simple_spread", ["--save-format", "tf1"]),     # the reference's checkpoint files, restored below
+    # the reference's constants as flags, and the debug NaN check on every training step
+    ("simple_spread", ["--tau", "0.05", "--grad-clip", "0.2", "--actor-reg", "0.01", "--buffer-size", "50000",
+                       "--check-nan"]),
 ])
 def test_train_cli_runs(tmp_path, capsys, scenario, extra):
     from experiments.train import parse_args, train

@@ -1029,3 +1029,31 @@ def test_facade_check_nan_raises_like_the_reference():
         eng.set_params(0, "actor", w)
         with pytest.raises(RuntimeError, match="Nan detected"):
             trainers[1].update(trainers, 200)
+
+
+def test_update_parity_non_default_constants():
+    """The reference's hard-coded constants as train.py flags (--tau, --grad-clip,
+    --actor-reg): one update per agent with tau 0.05, clip 0.2, actor
+    regulariser 1e-2 against the oracle run with the same constants."""
+    dims, B, L = [18, 18, 18], 512, 3000
+    c = synthetic_trainer_case(dims, B, L, seed=61)
+    tau, clip, reg = 0.05, 0.2, 1e-2
+    eng = Engine(dims, batch_size=B, capacity=L + 7, tau=tau, grad_clip=clip, actor_reg=reg)
+    eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
+    for i, p in enumerate(c["params"]):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            eng.set_params(i, w, p[w])
+    agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
+    for i in range(3):
+        eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
+                   u_act=torch.from_numpy(c["u_act"][i]))
+        got = eng.stats(i)
+        want, _ = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i],
+                                 grad_clip=clip, tau=tau, actor_reg=reg)
+        assert abs(got[0] - want[0]) <= 1e-5 * abs(want[0]) + 1e-7, (i, got[0], want[0])
+        assert abs(got[1] - want[1]) <= 2e-5 * abs(want[1]) + 2e-6, (i, got[1], want[1])   # p_loss uses reg
+        for w, ref in (("actor", agents[i].actor), ("tgt_actor", agents[i].tgt_actor),
+                       ("critic", agents[i].critic), ("tgt_critic", agents[i].tgt_critic)):
+            dev = eng.get_params(i, w)
+            for k in ref:
+                assert np.max(np.abs(dev[k] - ref[k].reshape(dev[k].shape))) < 2e-4, (i, w, k)

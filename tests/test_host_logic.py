@@ -66,6 +66,9 @@ def test_cli_flags_mirror_reference_defaults():
     assert (a.save_rate, a.load_dir, a.restore, a.display, a.benchmark) == (1000, "", False, False, False)
     assert (a.benchmark_iters, a.benchmark_dir, a.plots_dir) == (100000, "./benchmark_files/", "./learning_curves/")
     assert a.num_envs == 1          # default = the reference's single env
+    # its hard-coded constants, exposed with its values (maddpg.py:21,56,130,142,147)
+    assert (a.tau, a.grad_clip, a.actor_reg, a.buffer_size) == (1e-2, 0.5, 1e-3, 1000000)
+    assert a.check_nan is False
 
 
 @pytest.mark.parametrize("t0,t1,want", [(0, 1, 0), (99, 100, 1), (100, 101, 0), (0, 1024, 10),
