@@ -336,48 +336,16 @@ def exchange_limit_us(mode="strict", efficiency=0.8):
 
 
 def rank_launch_plan(gpus, environ, argv, port=None):
-    """How `bench.py --gpus N` becomes N ranks (pure host logic, tested on CPU).
-
-    * WORLD_SIZE set (torchrun / the driver's launch): it must equal --gpus,
-      else SystemExit(2) -- a line measured on another world size would be
-      reported under the wrong N;
-    * WORLD_SIZE unset and N > 1: the torchrun command that starts N fresh rank
-      processes of this script (one per GPU, rendezvous on 127.0.0.1), to run
-      as a child process before this one makes any GPU call;
-    * otherwise None: run here as the single rank."""
-    if gpus < 1:
-        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
-    ws = environ.get("WORLD_SIZE")
-    if ws is not None:
-        if int(ws) != gpus:
-            print(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}; refusing to report a {ws}-rank run as "
-                  f"n_gpus={gpus}", file=sys.stderr)
-            raise SystemExit(2)
-        return None
-    if gpus == 1:
-        return None
-    # the rendezvous store binds its own port (endpoint port 0: no probe-then-
-    # bind race with other jobs on a shared box); every address is 127.0.0.1
-    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-            "--rdzv-backend=c10d", f"--rdzv-endpoint=127.0.0.1:{int(port or 0)}", "--local-addr", "127.0.0.1",
-            os.path.join(ROOT, "bench.py")] + list(argv)
+    """How `bench.py --gpus N` becomes N ranks (maddpg_amd.launch: WORLD_SIZE set
+    must equal N; unset with N > 1: a torchrun child of N fresh rank processes;
+    otherwise None, this process is the single rank)."""
+    from maddpg_amd.launch import rank_launch_plan as plan
+    return plan(gpus, environ, os.path.join(ROOT, "bench.py"), argv, port, who="bench.py")
 
 
 def run_ranks(plan):
-    """run the torchrun child in its own process group; a SIGTERM / SIGINT to
-    this launcher (a time limit) is passed on to the whole group, so no rank
-    outlives it"""
-    import signal
-    child = subprocess.Popen(plan, cwd=ROOT, start_new_session=True)
-
-    def forward(sig, _frame):
-        try:
-            os.killpg(child.pid, sig)
-        except ProcessLookupError:
-            pass
-    for s in (signal.SIGTERM, signal.SIGINT):
-        signal.signal(s, forward)
-    return child.wait()
+    from maddpg_amd.launch import run_ranks as run
+    return run(plan, cwd=ROOT)
 
 
 def main():

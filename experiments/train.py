@@ -18,6 +18,7 @@ multiple of ``--save-rate`` and averages the last ``--save-rate`` entries
 host without a device sync.
 
     python experiments/train.py --scenario simple_spread --num-envs 1024 --exp-name spread
+    python experiments/train.py --scenario simple_spread --num-envs 4096 --num-gpus 8
     torchrun --nproc-per-node 8 experiments/train.py --scenario simple_spread --num-envs 4096
 """
 import argparse
@@ -77,6 +78,9 @@ def parse_args(argv=None):
                         help="debug: after every training step check every parameter, Adam slot and update stat "
                              "for NaN / Inf and stop with 'Nan detected' (the reference's _Function(check_nan), "
                              "tf_util.py:322,366-368)")
+    parser.add_argument("--num-gpus", type=int, default=None,
+                        help="start one rank per GPU from this command (torchrun child, 127.0.0.1 rendezvous); "
+                             "under torchrun it must equal WORLD_SIZE (default: torchrun's world, else 1)")
     parser.add_argument("--update-mode", choices=["strict", "throughput"], default="strict",
                         help="strict: the reference's update order; throughput: every agent's gradients from "
                              "the round-start parameters, then every optimizer step (SURVEY 8e, single GPU)")
@@ -281,5 +285,18 @@ def train(arglist):
     return runner
 
 
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    arglist = parse_args(argv)
+    if arglist.num_gpus is not None:
+        from maddpg_amd.launch import rank_launch_plan, run_ranks
+        plan = rank_launch_plan(arglist.num_gpus, os.environ, os.path.abspath(__file__), argv,
+                                who="train.py")
+        if plan is not None:          # N > 1 without torchrun: N rank processes, this one only waits
+            return run_ranks(plan)
+    train(arglist)
+    return 0
+
+
 if __name__ == '__main__':
-    train(parse_args())
+    sys.exit(main())

@@ -89,3 +89,30 @@ def test_scaling_prediction_model():
             prev = mid["env_steps_per_sec"]
         lim = bench.exchange_limit_us(mode)
         assert abs(bench.predict_scaling(8, mode, lim)["weak_scaling_efficiency"] - 0.8) < 1e-3
+
+
+# experiments/train.py --num-gpus N: the same launcher (maddpg_amd.launch)
+def _train(args, **env):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "experiments", "train.py")] + args, cwd=ROOT,
+                          env=e, capture_output=True, text=True, timeout=120)
+
+
+def test_train_num_gpus_plan():
+    from maddpg_amd.launch import rank_launch_plan
+    script = os.path.join(ROOT, "experiments", "train.py")
+    plan = rank_launch_plan(4, {}, script, ["--num-gpus", "4", "--num-envs", "64"], who="train.py")
+    assert plan[:3] == [sys.executable, "-m", "torch.distributed.run"] and "--nproc-per-node=4" in plan
+    assert plan[-5:] == [script, "--num-gpus", "4", "--num-envs", "64"]
+    assert rank_launch_plan(4, {"WORLD_SIZE": "4"}, script, []) is None
+    assert rank_launch_plan(1, {}, script, []) is None
+    with pytest.raises(SystemExit):
+        rank_launch_plan(0, {}, script, [])
+
+
+def test_train_num_gpus_disagreeing_with_torchrun_fails():
+    """under torchrun, --num-gpus must equal WORLD_SIZE: exit 2 before any import of torch"""
+    r = _train(["--num-gpus", "8"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert r.returncode == 2 and "refusing" in r.stderr and "train.py" in r.stderr
+    assert not r.stdout.strip()

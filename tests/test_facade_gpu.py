@@ -250,3 +250,29 @@ def test_train_cli_display_headless(tmp_path, capsys):
     assert sorted(os.listdir(d))[:2] == ["frame_00000.png", "frame_00001.png"]
     pos = np.load(os.path.join(d, "positions.npz"))["pos"]
     assert pos.shape == (7, 5, 2) and np.all(np.isfinite(pos))
+
+
+def test_train_cli_num_gpus_two_ranks(tmp_path):
+    """`python experiments/train.py --num-gpus 2` starts two rank processes itself
+    (maddpg_amd.launch, as bench.py --gpus does); on this one-GPU box both share
+    cuda:0 (MDP_SHARED_GPU=1, gloo group, the real xGMI exchange).  Rank 0 alone
+    prints the reference's lines and writes the curve; throughput counts both
+    ranks' env copies."""
+    import pickle
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MDP_SHARED_GPU="1", MDP_DP_XGMI="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "experiments", "train.py"), "--num-gpus", "2",
+                        "--scenario", "simple_spread", "--num-envs", "64", "--num-episodes", "300",
+                        "--save-rate", "100", "--batch-size", "64", "--max-episode-len", "5",
+                        "--save-dir", str(tmp_path) + "/", "--plots-dir", str(tmp_path) + "/", "--exp-name", "m"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = r.stdout
+    assert out.count("Starting iterations...") == 1 and out.count("...Finished total of") == 1, out[-2000:]
+    assert out.count("mean episode reward") == 3
+    assert out.rstrip().splitlines()[-1].startswith("throughput: ")
+    assert len(pickle.load(open(str(tmp_path) + "/m_rewards.pkl", "rb"))) == 3
