@@ -43,6 +43,10 @@ extern "C" {
 #define MDP_MAX_AGENTS 8
 #define MDP_ACT_DIM 5          /* MPE Discrete(dim_p*2+1) action spaces */
 #define MDP_MAX_UNITS 256      /* largest --num-units (train.py:24) */
+/* Besides these bounds, a configuration must fit the kernels' LDS envelope (a
+   16-row tile of every launch in a CU's 160 KB: the sum of obs dims up to
+   ~530 / ~470 / ~270 at 64 / 128 / 256 units); mdp_arena_bytes returns -1 and
+   mdp_create's handle carries the reason otherwise. */
 #define MDP_ABI_VERSION 5
 
 enum mdp_scenario {

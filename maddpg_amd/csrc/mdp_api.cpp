@@ -193,6 +193,23 @@ bool build_layout(const mdp_config* c, Layout& L, std::string& err) {
     std::memset(&L.env, 0, sizeof(L.env));
   }
   L.n_ent = n + L.env.n_landmarks;
+  // The kernels' envelope: one 16-row tile of every launch keeps its rows and
+  // activations in the CU's 160 KB of LDS.  The reference (TF1) has no such
+  // limit; its largest MPE case (simple_tag N=6, H=128) needs 66 KB.  A larger
+  // configuration is refused here, at create, not by its first update.
+  {
+    int need = std::max(lds_critic_bytes(T, 1), lds_actor_bytes(T));
+    need = std::max(need, lds_eval_bytes(std::max(cin_max, obs_max), H));
+    if (c->scenario != MDP_SCN_NONE) need = std::max(need, lds_rollout_bytes(T));
+    if (need > MDP_LDS_BUDGET) {
+      char b[200];
+      std::snprintf(b, sizeof(b),
+                    "configuration outside the kernels' LDS envelope: a 16-row tile needs %d bytes, a CU has %d "
+                    "(sum of obs dims %d, %d units)", need, MDP_LDS_BUDGET, sum_obs, c->num_units);
+      err = b;
+      return false;
+    }
+  }
   if (c->episode_log_rows < 0) { err = "episode_log_rows < 0"; return false; }
   // lockstep logging writes slot ep_base + e for every env finishing in one
   // step: a ring shorter than two steps' worth would overwrite records of the

@@ -76,7 +76,7 @@ class Engine:
         pt = ctypes.c_int64()
         nbytes = self.lib.mdp_arena_bytes(ctypes.byref(cfg), ctypes.byref(pt))
         if nbytes < 0:
-            raise ValueError("invalid maddpg configuration (see mdp_arena_bytes)")
+            raise ValueError(f"invalid maddpg configuration: {self._config_error(cfg)}")
         self.param_floats = pt.value
         with torch.cuda.device(self.device):
             self.arena = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
@@ -110,6 +110,15 @@ class Engine:
     def _c(self, name, *args):
         rc = getattr(self.lib, name)(self.h, *args)
         return _lib.check(self.lib, self.h, rc, name)
+
+    def _config_error(self, cfg):
+        """why mdp_arena_bytes refused `cfg`: mdp_create validates the same layout
+        first and keeps the message on the handle it returns (no GPU call)"""
+        h = ctypes.c_void_p()
+        self.lib.mdp_create(ctypes.byref(cfg), None, 0, None, ctypes.byref(h))
+        msg = self.lib.mdp_last_error(h).decode() if h.value else "mdp_create returned no handle"
+        self.lib.mdp_destroy(h)
+        return msg
 
     def close(self):
         if getattr(self, "h", None):

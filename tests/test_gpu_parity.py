@@ -304,6 +304,19 @@ def test_update_parity_tag6_h128_ragged():
     _update_parity([22, 22, 22, 22, 20, 20], B=1000, L=6000, seed=32, H=128)
 
 
+@pytest.mark.parametrize("dims,H,B,local_q", [
+    ([66] * 8, 64, 100, None),                       # 8 agents, critic input 568
+    ([95] * 3, 256, 80, [False, True, False]),       # H = 256, critic input 300, one DDPG critic
+    ([33] * 8, 256, 48, None),                       # 8 agents at H = 256
+])
+def test_update_parity_lds_envelope_edge(dims, H, B, local_q):
+    """the largest configurations the kernels' LDS envelope admits
+    (tests/test_host_logic.py LDS_EDGE: one more obs unit is refused at create)
+    train in parity with the oracle: the gradient tiles at ~160 KB of LDS and
+    the optimizer on nets of up to 150K parameters"""
+    _update_parity(dims, B=B, L=5 * B, seed=33 + H, local_q=local_q, H=H)
+
+
 @pytest.mark.parametrize("dims,local_q,B,H", [([18, 18, 18], None, 1024, 64),
                                               ([8, 10, 10], [True, False, False], 256, 64),
                                               ([22, 22, 20], None, 256, 128)])

@@ -56,6 +56,37 @@ def test_arena_size_and_config_validation():
     assert lib.mdp_arena_bytes(ctypes.byref(_cfg(scenario=0, num_envs=0)), None) > 0
 
 
+def _envelope_cfg(dims, units):
+    c = _cfg(scenario=0, num_envs=0, n_agents=len(dims), num_units=units)
+    for i, d in enumerate(dims):
+        c.obs_dim[i] = d
+    return c
+
+
+# the largest per-agent obs dim that fits the kernels' LDS envelope (measured
+# with mdp_arena_bytes): (agents, units) -> obs dim
+LDS_EDGE = {(8, 64): 66, (3, 256): 95, (8, 256): 33, (1, 256): 256}
+
+
+@pytest.mark.parametrize("n,units", sorted(LDS_EDGE))
+def test_lds_envelope_refused_at_create(n, units):
+    """A configuration whose 16-row tile does not fit a CU's LDS is refused by
+    mdp_arena_bytes / mdp_create with the reason, not by its first update; the
+    edge itself is accepted (tests/test_gpu_parity.py trains it)."""
+    lib = _lib.load()
+    edge = LDS_EDGE[(n, units)]
+    assert lib.mdp_arena_bytes(ctypes.byref(_envelope_cfg([edge] * n, units)), None) > 0
+    if edge == 256:                       # obs_dim's own range ends first
+        return
+    over = _envelope_cfg([edge + 1] * n, units)
+    assert lib.mdp_arena_bytes(ctypes.byref(over), None) < 0
+    h = ctypes.c_void_p()
+    assert lib.mdp_create(ctypes.byref(over), None, 0, None, ctypes.byref(h)) < 0
+    msg = lib.mdp_last_error(h).decode()
+    lib.mdp_destroy(h)
+    assert "LDS envelope" in msg and f"sum of obs dims {(edge + 1) * n}" in msg, msg
+
+
 def test_cli_flags_mirror_reference_defaults():
     from experiments.train import parse_args
     a = parse_args([])
