@@ -139,6 +139,32 @@ def test_act_and_q_values_match_oracle():
     np.testing.assert_allclose(q, nets.mlp_fwd(ag.tgt_critic, x)[0][:, 0], rtol=1e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("H", [64, 128])
+def test_device_gumbel_noise_is_the_pinned_philox(H):
+    """The device's own Gumbel noise (mdp_act without injected uniforms) is
+    Philox4x32-10 with the 23-bit float: every sampled action equals the
+    oracle's gumbel_softmax on oracle/philox.py's uniforms for the same
+    (seed, stream, counter, row) -- and that generator is pinned to the
+    Random123 known-answer vectors (tests/test_oracle.py).  The seed uses both
+    key words; 100 rows = 6 full tiles + a ragged one; the counter advances per
+    call (stream 0x40000 | agent << 1 | target, mdp_api.cpp mdp_act)."""
+    from oracle import philox
+    dims = [18, 18, 18]
+    seed = 0x9E3779B97F4A7C15
+    c = synthetic_trainer_case(dims, B=100, L=100, seed=13, H=H)
+    eng = Engine(dims, num_units=H, batch_size=100, capacity=200, seed=seed)
+    for i, p in enumerate(c["params"]):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
+            eng.set_params(i, w, p[w])
+    obs = c["data"][0][0][:100].astype(np.float32)
+    for k, (agent, target) in enumerate([(1, False), (1, True), (2, False), (0, True), (1, False)]):
+        got = eng.act(agent, torch.from_numpy(obs), target=target).cpu().numpy()
+        u = philox.uniforms5(seed, 0x40000 | (agent << 1) | int(target), k, np.arange(100))
+        ag = trainer.AgentParams(**c["params"][agent])
+        want = (trainer.target_act if target else trainer.act)(ag, obs, u)
+        np.testing.assert_allclose(got, want, atol=2e-6, err_msg=f"call {k}: agent {agent} target {target}")
+
+
 # ------------------------------------------------------------------ update
 def _device_grads(eng, agent, net):
     """the batch-reduced gradient the optimizer step of (agent, net) consumed
