@@ -687,20 +687,23 @@ __device__ inline void env_physics_tile(const EnvDesc& E, float* sp, float* sv, 
   __syncthreads();
 }
 
-// reset_world of one env from Philox uniforms
+// reset_world of one env from Philox uniforms.  Uniform slot c (2 per entity in
+// entity order, then the adversary goal) is word c % 4 of the Philox block at
+// counter (env, ctr, stream, c / 4); the slots are consumed in order, so each
+// block is generated when its first word is needed -- up to 2 MDP_MAX_ENT + 1
+// slots (an earlier revision kept a fixed 20 and read past it beyond 10 entities)
 __device__ inline void env_reset_one(const EnvDesc& E, uint64_t seed, uint32_t stream, uint32_t ctr, uint32_t env,
                                      float* p, float* v, int32_t* goal) {
   const int n = E.n_agents, ne = E.n_agents + E.n_landmarks;
-  uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-  float u[4 * 5];
-  for (int q = 0; q < 5; ++q) {
-    const uint4 r = Philox::gen(make_uint4(env, ctr, stream, (uint32_t)q), key);
-    u[4 * q] = u01(r.x);
-    u[4 * q + 1] = u01(r.y);
-    u[4 * q + 2] = u01(r.z);
-    u[4 * q + 3] = u01(r.w);
-  }
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  uint4 blk = make_uint4(0u, 0u, 0u, 0u);
   int c = 0;
+  auto next_u = [&]() -> float {
+    const int w = c & 3;
+    if (w == 0) blk = Philox::gen(make_uint4(env, ctr, stream, (uint32_t)(c >> 2)), key);
+    ++c;
+    return u01(w == 0 ? blk.x : w == 1 ? blk.y : w == 2 ? blk.z : blk.w);
+  };
   for (int e = 0; e < ne; ++e) {
     float lo = -1.f, hi = 1.f, sc = 1.f;
     if (e >= n) {
@@ -710,13 +713,15 @@ __device__ inline void env_reset_one(const EnvDesc& E, uint64_t seed, uint32_t s
         hi = 0.9f;
       }
     }
-    p[2 * e] = sc * (lo + (hi - lo) * u[c++]);
-    p[2 * e + 1] = sc * (lo + (hi - lo) * u[c++]);
+    const float ux = next_u();
+    const float uy = next_u();
+    p[2 * e] = sc * (lo + (hi - lo) * ux);
+    p[2 * e + 1] = sc * (lo + (hi - lo) * uy);
     v[2 * e] = 0.f;
     v[2 * e + 1] = 0.f;
   }
   if (E.scenario == MDP_SCN_ADVERSARY) {
-    int g = (int)(u[c] * E.n_landmarks);
+    int g = (int)(next_u() * E.n_landmarks);
     *goal = g < E.n_landmarks ? g : E.n_landmarks - 1;
   } else {
     *goal = 0;

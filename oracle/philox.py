@@ -68,3 +68,38 @@ def uniforms5(seed, stream, ctr, rows):
         out.append(philox4x32_10(c, key))
     a, b = out
     return u01(np.concatenate([a, b[:, :1]], 1))
+
+
+def slot_uniforms(seed, stream, ctr, envs, count):
+    """[len(envs), count] uniforms of mdp_kernels.hip env_reset_one: slot c is word
+    c % 4 of the block at counter (env, ctr, stream, c / 4)"""
+    envs = np.asarray(envs, np.uint64)
+    key = np.array([seed & MASK, (seed >> 32) & MASK], np.uint64)
+    blocks = []
+    for q in range((count + 3) // 4):
+        c = np.stack([envs, np.full_like(envs, ctr & MASK), np.full_like(envs, stream & MASK),
+                      np.full_like(envs, q)], -1)
+        blocks.append(philox4x32_10(c, key))
+    return u01(np.concatenate(blocks, 1)[:, :count])
+
+
+class ResetStream:
+    """an `rng` for oracle/mpe.py's Scenario.reset(rng, E) that serves the
+    device's reset uniforms: uniform() takes the next two slots per env in
+    call order (entity order), integers() the slot after every position (the
+    adversary goal, (int)(u * L) on the device)"""
+
+    def __init__(self, u, n_entities):
+        self.u, self.c, self.goal_slot = u, 0, 2 * n_entities
+
+    def uniform(self, lo, hi, size):
+        E, two = size
+        assert two == 2
+        lo32, span = np.float32(lo), np.float32(hi) - np.float32(lo)
+        out = lo32 + span * self.u[:, self.c:self.c + 2]
+        self.c += 2
+        return out.astype(np.float64)
+
+    def integers(self, lo, hi, size):
+        g = (self.u[:, self.goal_slot] * np.float32(hi - lo)).astype(np.int64)
+        return lo + np.minimum(g, hi - lo - 1)

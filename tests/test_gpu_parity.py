@@ -738,6 +738,35 @@ def test_env_step_parity(name, n, na):
     assert eng.buffer_len() == 3 * E
 
 
+@pytest.mark.parametrize("name,n,na", SCENARIOS + [("simple_adversary", 8, 1)])
+def test_env_reset_is_the_scenario_reset_on_pinned_philox(name, n, na):
+    """mdp_env_reset = the scenario's reset_world (oracle/mpe.py) drawing the
+    device's Philox uniforms (oracle/philox.py, KAT-pinned): every position to
+    fp32 rounding, velocities zero, the adversary goal exact.  The 8-agent
+    spread (16 entities, 32 uniform slots) and the 8-agent adversary (15
+    entities + the goal: 31 slots) need more than the 20 uniforms an earlier
+    revision of env_reset_one kept, which it then read past; two resets
+    advance the counter."""
+    from oracle import philox
+    from maddpg_amd.envs import spec
+    sp = spec(name, n, na if na else None)
+    E, seed = 37, 0x0123456789ABCDEF
+    eng = Engine(sp.obs_dims, batch_size=16, capacity=1000, num_envs=E, scenario=name,
+                 num_adversaries=sp.num_adversaries, max_episode_len=25, seed=seed)
+    sc = _oracle_scn(name, n, na)
+    ne = sc.n_entities
+    for k in range(2):
+        eng.env_reset()
+        st = eng.env_state()
+        u = philox.slot_uniforms(seed, 0x30000, k, np.arange(E), 2 * ne + 1)
+        want = sc.reset(philox.ResetStream(u, ne), E)
+        np.testing.assert_allclose(st["pos"], want["pos"], rtol=0, atol=1e-6, err_msg=f"reset {k}")
+        assert np.all(st["vel"] == 0) and np.all(st["ep_step"] == 0)
+        if name == "simple_adversary":
+            np.testing.assert_array_equal(st["goal"], want["goal"])
+            assert len(set(st["goal"].tolist())) > 1
+
+
 def test_env_episode_reset_and_log():
     from maddpg_amd.envs import spec
     sp = spec("simple_spread")
