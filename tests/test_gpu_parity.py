@@ -808,6 +808,44 @@ def test_rollout_policy_actions_match_oracle():
         np.testing.assert_allclose(rows[:, lay[j]["act"]:lay[j]["act"] + ACT], want, atol=2e-6)
 
 
+@pytest.mark.parametrize("name,n,na,H", [("simple_spread", 3, 0, 64), ("simple_tag", 6, 4, 128),
+                                         ("simple_adversary", 8, 1, 64)])
+def test_rollout_own_noise_and_episode_reset_are_pinned_philox(name, n, na, H):
+    """k_rollout without injected uniforms: every stored action is the oracle's
+    gumbel-softmax of the device actor on the stored obs with the KAT-pinned
+    Philox uniforms of (seed, stream 0x10000 | agent, counter = vector step,
+    row = env), and the episode end's env.reset() (train.py:127-133) is the
+    scenario's reset_world on stream 0x20000 at the terminal step's counter."""
+    from oracle import philox
+    from maddpg_amd.envs import spec
+    sp = spec(name, n, na if na else None)
+    E, seed, T = 37, 0xDEADBEEF12345678, 3
+    eng = Engine(sp.obs_dims, num_units=H, batch_size=16, capacity=1000, num_envs=E, scenario=name,
+                 num_adversaries=sp.num_adversaries, max_episode_len=T, seed=seed)
+    eng.init_params(4)
+    eng.env_reset()
+    lay, _ = row_layout(sp.obs_dims)
+    actors = [eng.get_params(j, "actor") for j in range(n)]
+    for k in range(T):
+        eng.env_step()
+        rows = eng.replay_rows(k * E, E).cpu().numpy()
+        for j in range(n):
+            o = sp.obs_dims[j]
+            logits = nets.mlp_fwd(actors[j], rows[:, lay[j]["obs"]:lay[j]["obs"] + o])[0]
+            u = philox.uniforms5(seed, 0x10000 | j, k, np.arange(E))
+            np.testing.assert_allclose(rows[:, lay[j]["act"]:lay[j]["act"] + ACT], nets.gumbel_softmax(logits, u),
+                                       atol=2e-6, err_msg=f"step {k} agent {j}")
+    st = eng.env_state()
+    assert np.all(st["ep_step"] == 0) and eng.episode_count() == E
+    sc = _oracle_scn(name, n, na)
+    ne = sc.n_entities
+    want = sc.reset(philox.ResetStream(philox.slot_uniforms(seed, 0x20000, T - 1, np.arange(E), 2 * ne + 1), ne), E)
+    np.testing.assert_allclose(st["pos"], want["pos"], rtol=0, atol=1e-6)
+    assert np.all(st["vel"] == 0)
+    if name == "simple_adversary":
+        np.testing.assert_array_equal(st["goal"], want["goal"])
+
+
 @pytest.mark.parametrize("scenario,adv_policy,cap,general", [
     ("simple_spread", "maddpg", 20000, False),
     ("simple_spread", "maddpg", 3300, False),
