@@ -828,6 +828,7 @@ def test_rollout_own_noise_and_episode_reset_are_pinned_philox(name, n, na, H):
     actors = [eng.get_params(j, "actor") for j in range(n)]
     for k in range(T):
         eng.env_step()
+        eng.synchronize()       # no injected tensors: the step did not order torch's stream after it
         rows = eng.replay_rows(k * E, E).cpu().numpy()
         for j in range(n):
             o = sp.obs_dims[j]
