@@ -198,10 +198,23 @@ def _clip_mode_distance(eng, c, i, dgs):
     return out
 
 
-def _update_parity(dims, B, L, seed, local_q=None, H=64, check_round=True):
+def _philox_case_noise(c, n, B, key):
+    """the uniforms the device draws itself in agent i's strict update (counter
+    upd_ctr = i on a fresh engine): target actor j on stream (i << 8) | (j + 1),
+    the actor-loss sample on (i << 8) | 0x80, row = batch row (mdp_grads*.hip)"""
+    from oracle import philox
+    rows = np.arange(B)
+    c["u_tgt"] = [np.stack([philox.uniforms5(key, (i << 8) | (j + 1), i, rows) for j in range(n)]) for i in range(n)]
+    c["u_act"] = [philox.uniforms5(key, (i << 8) | 0x80, i, rows) for i in range(n)]
+
+
+def _update_parity(dims, B, L, seed, local_q=None, H=64, check_round=True, device_noise_key=None):
     c = synthetic_trainer_case(dims, B, L, seed, local_q, H)
     n = len(dims)
-    eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L + 7)
+    kw = {} if device_noise_key is None else {"seed": device_noise_key}
+    if device_noise_key is not None:
+        _philox_case_noise(c, n, B, device_noise_key)
+    eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L + 7, **kw)
     eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
     for i, p in enumerate(c["params"]):
         for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
@@ -209,8 +222,11 @@ def _update_parity(dims, B, L, seed, local_q=None, H=64, check_round=True):
     agents = [trainer.AgentParams(**copy.deepcopy(p), local_q=c["local_q"][i]) for i, p in enumerate(c["params"])]
     report, greport, wreport, creport = [], [], [], []
     for i in range(n if check_round else 1):
-        eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
-                   u_act=torch.from_numpy(c["u_act"][i]))
+        if device_noise_key is None:
+            eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
+                       u_act=torch.from_numpy(c["u_act"][i]))
+        else:                                     # the device's own Philox noise
+            eng.update(i, idx=torch.from_numpy(c["idx"][i]))
         got = eng.stats(i)
         want, og = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i])
         conditioned = {}
@@ -328,6 +344,21 @@ def test_update_parity_general_ragged_batch(monkeypatch):
 def test_update_parity_tag6_h128_ragged():
     # tag N=6 at H=128, B = 1000: the work-queue layer phase over 62 row tiles + 8 rows
     _update_parity([22, 22, 22, 22, 20, 20], B=1000, L=6000, seed=32, H=128)
+
+
+@pytest.mark.parametrize("dims,H,B,local_q,general", [
+    ([18, 18, 18], 64, 1024, None, False),                           # S2 shape, register-resident kernels
+    ([8, 10, 10], 64, 512, [True, False, False], False),             # a DDPG critic: its own target actor only
+    ([18, 18, 18], 64, 200, None, True),                             # general kernels, ragged
+    ([22, 22, 22, 22, 20, 20], 128, 256, None, False),               # tag N=6, H=128
+])
+def test_update_parity_device_noise_is_pinned_philox(monkeypatch, dims, H, B, local_q, general):
+    """mdp_update drawing its own Gumbel noise (no injected uniforms) is the
+    oracle update on the KAT-pinned Philox uniforms of each agent's streams at
+    counter i (agent i's update on a fresh engine), both key words in use"""
+    if general:
+        monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
+    _update_parity(dims, B=B, L=4 * B, seed=40 + B, local_q=local_q, H=H, device_noise_key=0xC0FFEE0123456789)
 
 
 @pytest.mark.parametrize("dims,H,B,local_q", [
@@ -1152,8 +1183,11 @@ def test_update_parity_non_default_constants():
             eng.set_params(i, w, p[w])
     agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
     for i in range(3):
-        eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
-                   u_act=torch.from_numpy(c["u_act"][i]))
+        if device_noise_key is None:
+            eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
+                       u_act=torch.from_numpy(c["u_act"][i]))
+        else:                                     # the device's own Philox noise
+            eng.update(i, idx=torch.from_numpy(c["idx"][i]))
         got = eng.stats(i)
         want, _ = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i],
                                  grad_clip=clip, tau=tau, actor_reg=reg)
