@@ -439,16 +439,34 @@ def test_throughput_mode_round_parity(monkeypatch, dims, local_q, B, H, general)
     Polyak (mdp_update_all) vs oracle.trainer.update_round_throughput on the
     same injected indices and uniforms: critic loss within 1e-5 relative,
     parameters within the fp32 tolerance of the strict-mode parity test."""
+    _throughput_round_parity(monkeypatch, dims, local_q, B, H, general)
+
+
+@pytest.mark.parametrize("dims,local_q,B,H,general", [
+    ([18, 18, 18], None, 1024, 64, False), ([8, 10, 10], [True, False, False], 256, 64, True),
+    ([22, 22, 22, 22, 20, 20], None, 1000, 128, False)])
+def test_throughput_mode_device_noise_is_pinned_philox(monkeypatch, dims, local_q, B, H, general):
+    """the same round drawing its own noise: agent i at counter upd_ctr + i
+    (mdp_grads*.hip), i.e. the KAT-pinned Philox streams of strict mode's
+    agent i on a fresh engine"""
+    _throughput_round_parity(monkeypatch, dims, local_q, B, H, general, device_noise_key=0x5EED5EED00C0FFEE)
+
+
+def _throughput_round_parity(monkeypatch, dims, local_q, B, H, general, device_noise_key=None):
     if general:
         monkeypatch.setenv("MDP_GENERAL_GRADS", "1")
     L = 3000
     c = synthetic_trainer_case(dims, B, L, seed=61, local_q=local_q, H=H)
+    if device_noise_key is not None:
+        _philox_case_noise(c, len(dims), B, device_noise_key)
+        c["u_tgt"], c["u_act"] = np.stack(c["u_tgt"]), np.stack(c["u_act"])
     # no batch row with a ReLU input within 1e-5 of its layer's scale of zero: there two
     # correct fp32 evaluations may mask differently (see relu_margin_clean_idx; at B = 4096
     # the unconditioned batch flips one mask of agent 2's actor step, 7e-4 of max|g|)
     relu_margin_clean_idx(c)
     n = len(dims)
-    eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L + 7)
+    kw = {} if device_noise_key is None else {"seed": device_noise_key}
+    eng = Engine(dims, c["local_q"], num_units=H, batch_size=B, capacity=L + 7, **kw)
     eng.add_rows(torch.from_numpy(joint_rows(c["data"], dims)))
     for i, p in enumerate(c["params"]):
         for w in ("actor", "critic", "tgt_actor", "tgt_critic"):
@@ -471,8 +489,11 @@ def test_throughput_mode_round_parity(monkeypatch, dims, local_q, B, H, general)
         og64 = round_grads()
     finally:
         nets.F32, trainer.F32 = old32
-    eng.update_all(idx=torch.from_numpy(c["idx"]), u_tgt=torch.from_numpy(c["u_tgt"]),
-                   u_act=torch.from_numpy(c["u_act"]))
+    if device_noise_key is None:
+        eng.update_all(idx=torch.from_numpy(c["idx"]), u_tgt=torch.from_numpy(c["u_tgt"]),
+                       u_act=torch.from_numpy(c["u_act"]))
+    else:                                         # the device's own Philox noise
+        eng.update_all(idx=torch.from_numpy(c["idx"]))
     want = trainer.update_round_throughput(agents, c["data"], c["idx"], c["u_tgt"], c["u_act"])
     tworst, gworst, cworst = 0.0, 0.0, 0.0
     for i in range(n):
