@@ -1204,11 +1204,8 @@ def test_update_parity_non_default_constants():
             eng.set_params(i, w, p[w])
     agents = [trainer.AgentParams(**copy.deepcopy(p)) for p in c["params"]]
     for i in range(3):
-        if device_noise_key is None:
-            eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
-                       u_act=torch.from_numpy(c["u_act"][i]))
-        else:                                     # the device's own Philox noise
-            eng.update(i, idx=torch.from_numpy(c["idx"][i]))
+        eng.update(i, idx=torch.from_numpy(c["idx"][i]), u_tgt=torch.from_numpy(c["u_tgt"][i]),
+                   u_act=torch.from_numpy(c["u_act"][i]))
         got = eng.stats(i)
         want, _ = trainer.update(agents, i, c["data"], c["idx"][i], c["u_tgt"][i], c["u_act"][i],
                                  grad_clip=clip, tau=tau, actor_reg=reg)
