@@ -63,7 +63,6 @@ __global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ r
   }
 }
 
-// ring append of whole rows: replay[(next + r) % cap] = src[r]
 // ============================================================= check_nan
 // non-finite entries of a float span -- the reference's _Function(check_nan)
 // (tf_util.py:322,366-368) as an opt-in debug check (mdp_check_finite):
@@ -76,6 +75,7 @@ __global__ __launch_bounds__(256) void k_count_nonfinite(const float* __restrict
   if (c) atomicAdd(cnt, c);
 }
 
+// ring append of whole rows: replay[(next + r) % cap] = src[r]
 __global__ __launch_bounds__(256) void k_put_rows(float* __restrict__ replay, int stride, int64_t cap,
                                                   int64_t next, const float* __restrict__ src, int64_t rows) {
   const int v4 = stride >> 2;

@@ -32,6 +32,7 @@ def curve(scenario, num_envs, episodes, seed=0, num_agents=None, scenario_advers
         n = r.episodes()
         rew = r.episode_rewards(n - num_envs, num_envs)
         out.append(float(rew[:, 0].mean()))
+        print(f"{len(out)} {out[-1]:.3f} rounds {rounds}", file=sys.stderr, flush=True)
     return {"scenario": scenario, "num_envs": num_envs, "episodes_per_point": num_envs,
             "points": len(out), "transitions": episodes * max_episode_len * num_envs, "update_rounds": rounds,
             "seconds": round(time.time() - t0, 2), "mean_episode_reward": [round(v, 3) for v in out]}
