@@ -65,11 +65,12 @@ def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, m
     episode_step = 0
     train_step = prefill
     env_steps = updates = 0
+    ep_rew, episode_rewards = 0.0, []                              # train.py:121-124
     t0 = time.perf_counter()
     while True:
         action_n = []
         for i in range(n):                                         # train.py:112
-            u = rng.random((1, 5)).astype(np.float32)
+            u = rng.random((1, 5), dtype=np.float32)                   # [0, 1) like tf.random_uniform
             action_n.append(trainer.act(agents[i], obs_n[i][0:1], u)[0])
         st, new_obs_n, rew = sc.step(st, np.array(action_n)[None])  # :114
         episode_step += 1
@@ -77,7 +78,10 @@ def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, m
         for i in range(n):                                         # :119-120
             bufs[i].add(obs_n[i][0], action_n[i], float(rew[0, i]), new_obs_n[i][0], 0.0)
         obs_n = new_obs_n
+        ep_rew += float(rew[0].sum())
         if terminal:                                               # :127-128
+            episode_rewards.append(ep_rew)
+            ep_rew = 0.0
             st = sc.reset(rng, 1)
             obs_n = sc.observation(st)
             episode_step = 0
@@ -90,8 +94,10 @@ def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, m
             batch_n = [bufs[j].sample_index(idx) for j in range(n)]
             own = bufs[i].sample_index(idx)
             batch_n[i] = own
-            u_tgt = rng.random((n, batch_size, 5)).astype(np.float32)
-            u_act = rng.random((batch_size, 5)).astype(np.float32)
+            # fp32 draws in [0, 1): a float64 draw cast to fp32 rounds to 1.0 about
+            # once in 3e7 draws, and u = 1 makes -log(-log u) infinite (NaN actions)
+            u_tgt = rng.random((n, batch_size, 5), dtype=np.float32)
+            u_act = rng.random((batch_size, 5), dtype=np.float32)
             trainer.update_batch(agents, i, batch_n, u_tgt, u_act, gamma)
             updates += 1
         el = time.perf_counter() - t0
@@ -100,7 +106,8 @@ def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, m
     el = time.perf_counter() - t0
     return {"env_steps_per_sec": env_steps / el, "trainer_updates_per_sec": updates / el,
             "env_steps": env_steps, "updates": updates, "seconds": el, "scenario": scenario,
-            "batch_size": batch_size, "num_units": num_units, "prefill": prefill, "n_agents": n}
+            "batch_size": batch_size, "num_units": num_units, "prefill": prefill, "n_agents": n,
+            "episode_rewards": episode_rewards}
 
 
 def main():

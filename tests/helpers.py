@@ -71,8 +71,10 @@ def synthetic_trainer_case(dims, B, L, seed, local_q=None, H=64):
                            tgt_actor=nets.xavier_init(rng, dims[i], ACT, H),
                            tgt_critic=nets.xavier_init(rng, cin, 1, H)))
     idx = rng.integers(0, L, size=(n, B)).astype(np.int32)
-    u_tgt = rng.uniform(1e-6, 1.0, size=(n, n, B, ACT)).astype(np.float32)
-    u_act = rng.uniform(1e-6, 1.0, size=(n, B, ACT)).astype(np.float32)
+    # (a float64 draw near 1 rounds to 1.0 in fp32, where -log(-log u) is infinite: capped below 1)
+    top = np.nextafter(np.float32(1), np.float32(0))
+    u_tgt = np.minimum(rng.uniform(1e-6, 1.0, size=(n, n, B, ACT)).astype(np.float32), top)
+    u_act = np.minimum(rng.uniform(1e-6, 1.0, size=(n, B, ACT)).astype(np.float32), top)
     return dict(data=data, params=params, idx=idx, u_tgt=u_tgt, u_act=u_act, local_q=local_q)
 
 
