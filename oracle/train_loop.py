@@ -36,18 +36,20 @@ def make_scenario(name, n_agents=None, n_adv=None):
 
 
 def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, max_episode_len=25,
-        seed=0, prefill=None, gamma=0.95, max_steps=None):
+        seed=0, prefill=None, gamma=0.95, max_steps=None, local_q=None):
     sc = make_scenario(scenario)
     n = sc.n_agents
     dims = sc.obs_dims()
     rng = np.random.default_rng(seed)
     S = sum(dims)
     agents = []
+    local_q = [False] * n if local_q is None else list(local_q)     # train.py:67-74 (ddpg: local critic)
     for i in range(n):
-        cin = S + 5 * n
+        cin = dims[i] + 5 if local_q[i] else S + 5 * n
         agents.append(trainer.AgentParams(
             nets.xavier_init(rng, dims[i], 5, num_units), nets.xavier_init(rng, cin, 1, num_units),
-            nets.xavier_init(rng, dims[i], 5, num_units), nets.xavier_init(rng, cin, 1, num_units)))
+            nets.xavier_init(rng, dims[i], 5, num_units), nets.xavier_init(rng, cin, 1, num_units),
+            local_q=local_q[i]))
     bufs = [ReplayBuffer(1e6) for _ in range(n)]
     g = MT19937(seed)
     gate = batch_size * max_episode_len
@@ -65,7 +67,7 @@ def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, m
     episode_step = 0
     train_step = prefill
     env_steps = updates = 0
-    ep_rew, episode_rewards = 0.0, []                              # train.py:121-124
+    ep_rew, episode_rewards = np.zeros(n), []                      # train.py:121-124 (per agent)
     t0 = time.perf_counter()
     while True:
         action_n = []
@@ -78,10 +80,10 @@ def run(scenario="simple_spread", seconds=15.0, batch_size=1024, num_units=64, m
         for i in range(n):                                         # :119-120
             bufs[i].add(obs_n[i][0], action_n[i], float(rew[0, i]), new_obs_n[i][0], 0.0)
         obs_n = new_obs_n
-        ep_rew += float(rew[0].sum())
+        ep_rew += rew[0]
         if terminal:                                               # :127-128
-            episode_rewards.append(ep_rew)
-            ep_rew = 0.0
+            episode_rewards.append([float(ep_rew.sum())] + [float(v) for v in ep_rew])
+            ep_rew = np.zeros(n)
             st = sc.reset(rng, 1)
             obs_n = sc.observation(st)
             episode_step = 0

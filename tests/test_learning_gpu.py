@@ -21,9 +21,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _curve(scenario, batches, seed=0, num_envs=1024, update_mode="strict"):
+def _curve(scenario, batches, seed=0, num_envs=1024, update_mode="strict", per_agent=False, **runner_kw):
+    """mean total episode reward of each lockstep batch of num_envs episodes
+    (per_agent: [batch][1 + n], the total then every agent's own)"""
     from maddpg_amd.runner import VecRunner
-    r = VecRunner(scenario, num_envs, seed=seed, episode_log_rows=4 * num_envs)
+    r = VecRunner(scenario, num_envs, seed=seed, episode_log_rows=4 * num_envs, **runner_kw)
     if update_mode != "strict":
         r.eng.set_update_mode(update_mode)
     out = []
@@ -35,8 +37,8 @@ def _curve(scenario, batches, seed=0, num_envs=1024, update_mode="strict"):
         assert n == len(out) * num_envs + num_envs
         rew = r.episode_rewards(n - num_envs, num_envs)
         assert np.all(np.isfinite(rew))
-        out.append(float(rew[:, 0].mean()))
-    return out
+        out.append(rew.mean(0).astype(float) if per_agent else float(rew[:, 0].mean()))
+    return np.array(out) if per_agent else out
 
 
 @pytest.mark.parametrize("seed", [0, 1])
@@ -83,3 +85,24 @@ def test_spread_curve_tracks_the_reference_call_structure():
     ref = np.array(_fixture("simple_spread", 0))
     assert abs(np.mean(dev[4:]) - np.mean(ref[4:])) < 35.0, (dev, ref)
     assert np.max(np.abs(dev[4:] - ref[4:])) < 60.0, (dev, ref)
+
+
+def _fixture_agents(name, seed):
+    import json
+    import os
+    p = os.path.join(os.path.dirname(__file__), "golden", f"learning_{name}_s{seed}.json")
+    with open(p) as f:
+        return np.array(json.load(f)["mean_agent_reward"])
+
+
+def test_adversary_ddpg_curve_tracks_the_reference_call_structure():
+    """BASELINE configs[3]'s policies (simple_adversary, the adversary on DDPG's
+    local critic, the two good agents on MADDPG) against the oracle's one-env
+    loop, agent by agent (seed 0, 16 batches; oracle adversary -26.0 -> -9.5,
+    good agents +4.8 -> +7.3; the device measured within ~1 of it batch by
+    batch from batch 2 on)."""
+    dev = _curve("simple_adversary", 16, per_agent=True, num_adversaries=1, adv_policy="ddpg")[:, 1:]
+    ref = _fixture_agents("simple_adversary_ddpg", 0)
+    assert ref[0, 0] < -20.0 and np.mean(ref[2:, 0]) > -11.0          # the fixture shows the adversary learning
+    assert np.all(np.abs(dev[2:].mean(0) - ref[2:].mean(0)) < 1.5), (dev, ref)
+    assert np.max(np.abs(dev[2:] - ref[2:])) < 3.0, (dev, ref)

@@ -19,14 +19,15 @@ sys.path.insert(0, ROOT)
 
 
 def curve(scenario, num_envs, episodes, seed=0, num_agents=None, scenario_adversaries=None,
-          num_adversaries=0, max_episode_len=25, batch_size=1024, num_units=64, update_mode="strict"):
+          num_adversaries=0, max_episode_len=25, batch_size=1024, num_units=64, update_mode="strict",
+          adv_policy="maddpg"):
     from maddpg_amd.runner import VecRunner
     r = VecRunner(scenario, num_envs, n_agents=num_agents, scenario_adversaries=scenario_adversaries,
-                  num_adversaries=num_adversaries, batch_size=batch_size, num_units=num_units, seed=seed,
+                  num_adversaries=num_adversaries, adv_policy=adv_policy, batch_size=batch_size, num_units=num_units, seed=seed,
                   max_episode_len=max_episode_len, episode_log_rows=4 * num_envs)
     if update_mode != "strict":
         r.eng.set_update_mode(update_mode)
-    out, rounds, t0 = [], 0, time.time()
+    out, agents, rounds, t0 = [], [], 0, time.time()
     for _ in range(episodes):
         for _ in range(max_episode_len):
             rounds += r.step()
@@ -34,10 +35,12 @@ def curve(scenario, num_envs, episodes, seed=0, num_agents=None, scenario_advers
         n = r.episodes()
         rew = r.episode_rewards(n - num_envs, num_envs)
         out.append(float(rew[:, 0].mean()))
+        agents.append([round(float(v), 3) for v in rew[:, 1:].mean(0)])
         print(f"{len(out)} {out[-1]:.3f} rounds {rounds}", file=sys.stderr, flush=True)
     return {"scenario": scenario, "update_mode": update_mode, "seed": seed, "num_envs": num_envs, "episodes_per_point": num_envs,
             "points": len(out), "transitions": episodes * max_episode_len * num_envs, "update_rounds": rounds,
-            "seconds": round(time.time() - t0, 2), "mean_episode_reward": [round(v, 3) for v in out]}
+            "seconds": round(time.time() - t0, 2), "mean_episode_reward": [round(v, 3) for v in out],
+            "mean_agent_reward": agents}
 
 
 def main():
@@ -49,10 +52,11 @@ def main():
     ap.add_argument("--num-agents", type=int, default=None)
     ap.add_argument("--scenario-adversaries", type=int, default=None)
     ap.add_argument("--num-adversaries", type=int, default=0)
+    ap.add_argument("--adv-policy", default="maddpg")
     ap.add_argument("--update-mode", choices=["strict", "throughput"], default="strict")
     a = ap.parse_args()
     print(json.dumps(curve(a.scenario, a.num_envs, a.episodes, a.seed, a.num_agents, a.scenario_adversaries,
-                           a.num_adversaries, update_mode=a.update_mode)), flush=True)
+                           a.num_adversaries, update_mode=a.update_mode, adv_policy=a.adv_policy)), flush=True)
 
 
 if __name__ == "__main__":
