@@ -106,3 +106,19 @@ def test_adversary_ddpg_curve_tracks_the_reference_call_structure():
     assert ref[0, 0] < -20.0 and np.mean(ref[2:, 0]) > -11.0          # the fixture shows the adversary learning
     assert np.all(np.abs(dev[2:].mean(0) - ref[2:].mean(0)) < 1.5), (dev, ref)
     assert np.max(np.abs(dev[2:] - ref[2:])) < 3.0, (dev, ref)
+
+
+def test_tag_curve_tracks_the_reference_call_structure():
+    """simple_tag (3 adversaries + 1 good agent, all MADDPG) against the
+    oracle's one-env loop (seed 0, 16 batches).  Competitive: in both the
+    adversaries first learn to catch (their per-agent reward peaks at ~30 in
+    batches 4-7) and the good agent then learns to evade (adversaries back to
+    ~9-10, the good agent ~-12 to -15 by batches 12-15); the peak's batch
+    differs by a couple of batches, so the check is the peak's height and the
+    late level, agent by agent."""
+    dev = _curve("simple_tag", 16, per_agent=True)[:, 1:]
+    ref = _fixture_agents("simple_tag", 0)
+    for c in (dev, ref):
+        assert np.max(c[3:10, 0]) > 20.0, c          # the adversaries' catching phase
+        assert np.mean(c[12:, 0]) < 15.0, c          # then the good agent evades
+    assert np.all(np.abs(dev[12:].mean(0) - ref[12:].mean(0)) < 5.0), (dev, ref)
