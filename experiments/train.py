@@ -244,12 +244,19 @@ def train(arglist):
     vec_steps = 0
     say('Starting iterations...')
     from maddpg_amd.common.tf_util import check_nan
+    # one episode of every env copy (L vector steps, the steps without a round
+    # included) as one graph replay; --check-nan looks after every step
+    group = L if (L <= 64 and not arglist.check_nan) else 1
     while True:
-        if runner.step() and arglist.check_nan:
-            check_nan(runner.eng)
-        vec_steps += 1
-        if vec_steps % L:
-            continue
+        if group > 1:
+            runner.steps(group)
+            vec_steps += group
+        else:
+            if runner.step() and arglist.check_nan:
+                check_nan(runner.eng)
+            vec_steps += 1
+            if vec_steps % L:
+                continue
         # every env copy just terminated (train.py:116,127): E new episodes
         steps = vec_steps * E
         points = curve.finish(E, runner.episode_rewards if rank == 0 else None)

@@ -2318,13 +2318,13 @@ int mdp_train_steps(mdp_handle* h, int32_t n, const int32_t* rounds, int32_t lau
   if (need_env(h)) return -1;
   if (n < 1 || n > 64 || !rounds) return fail(h, "mdp_train_steps: 1 <= n <= 64 steps");
   std::vector<int> ks(rounds, rounds + n);
-  bool all_train = true;
-  for (int k : ks) {
+  for (int k : ks)
     if (k < 0 || k > 64) return fail(h, "mdp_train_steps: rounds must be in [0, 64]");
-    all_train = all_train && k > 0;
-  }
+  // steps without a round (replay below the gate, or fewer than train_every
+  // transitions per step: E = 1 trains every 100th step) are their rollout
+  // launch alone inside the group's graph
   const bool no_graph = h->comm && !h->dp_graphs;
-  const bool graphable = h->graphs && !no_graph && !any_prof(h) && h->eager_steps >= 1 && all_train;
+  const bool graphable = h->graphs && !no_graph && !any_prof(h) && h->eager_steps >= 1;
   if (!launch) {  // capture and instantiate ahead of time (nothing runs)
     hipGraphExec_t x = nullptr;
     return graphable ? multi_graph(h, ks, &x) : 0;

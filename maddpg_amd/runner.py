@@ -115,24 +115,22 @@ class VecRunner:
 
     def plan(self, n, skip=0):
         """the update rounds of vector steps skip .. skip + n - 1 from now (the
-        cadence of step()), or None when one of them would not train (replay
-        below the gate)"""
+        cadence of step(); 0 for a step that does not train: replay below the
+        gate, or no multiple of train_every crossed)"""
         ks, t, ln = [], self.train_step, self.eng.buffer_len()
         for i in range(skip + n):
             ln = min(self.eng.capacity, ln + self.num_envs)
             k = 0 if ln < self.gate else rounds_due(t, t + self.num_envs, self.train_every)
             t += self.num_envs
-            if i < skip:
-                continue
-            if k == 0:
-                return None
-            ks.append(k)
+            if i >= skip:
+                ks.append(k)
         return ks
 
     def steps(self, n):
-        """n vector steps as one graph replay (mdp_train_steps) when every one of
-        them trains (single GPU or the native exchanges); otherwise step() n
-        times.  Returns the update rounds run."""
+        """n (<= 64) vector steps as one graph replay (mdp_train_steps: the steps
+        that do not train are their rollout launch alone) on a single GPU or
+        the native exchanges; otherwise step() n times.  Returns the update
+        rounds run."""
         ks = self.plan(n) if (self.world_size == 1 or self.native_dp) else None
         if ks is None:
             return sum(self.step() for _ in range(n))

@@ -1016,6 +1016,47 @@ def test_train_steps_group_graph_equals_step_graphs(monkeypatch, general):
     assert a.episodes() == b.episodes()
 
 
+@pytest.mark.parametrize("E,every,gate_open", [(64, 100, True), (1, 100, True), (64, 100, False)])
+def test_train_steps_group_with_rollout_only_steps(E, every, gate_open):
+    """Groups whose steps do not all train (64 transitions per step and a round
+    per 100: rounds 1, 0, 1, 1, 0, ...; E = 1, the reference's own structure:
+    one round in 100 steps; a group that starts below the replay gate): the
+    group graph == the steps one by one, bit for bit, and the episode log."""
+    from maddpg_amd.runner import VecRunner
+
+    def make():
+        r = VecRunner("simple_spread", E, batch_size=64, capacity=2000, seed=11, train_every=every)
+        if gate_open:
+            r.prefill()
+            while r.step() == 0:              # the one eager training step
+                pass
+        return r
+
+    a, b = make(), make()
+    n = 120 if E == 1 else 12                 # E = 1: the next round is 100 steps after the eager one
+    pa_ = a.plan(n)
+    assert 0 in pa_ and (not gate_open or any(pa_)), pa_
+    if gate_open:
+        sizes = a.prepare_steps(n, 60 if E == 1 else 6)
+    else:                                     # below the gate: no eager step yet, groups fall back to one by one
+        sizes = [6] * (n // 6)
+    ra = sum(a.steps(g) for g in sizes)
+    rb = sum(b.step() for _ in range(n))
+    assert ra == rb and a.train_step == b.train_step and a.rounds == b.rounds
+    a.eng.synchronize()
+    b.eng.synchronize()
+    for i in range(a.n):
+        for w in ("actor", "critic", "tgt_actor", "tgt_critic", "m_actor", "v_critic"):
+            pa, pb = a.eng.get_params(i, w), b.eng.get_params(i, w)
+            for key in pa:
+                np.testing.assert_array_equal(pa[key], pb[key])
+    np.testing.assert_array_equal(a.eng.replay_rows(0, 2000).cpu().numpy(), b.eng.replay_rows(0, 2000).cpu().numpy())
+    assert a.eng.buffer_len() == b.eng.buffer_len()
+    np.testing.assert_array_equal(a.eng.get_rng_state(), b.eng.get_rng_state())
+    assert a.episodes() == b.episodes()
+    np.testing.assert_array_equal(a.episode_rewards(0, a.episodes()), b.episode_rewards(0, b.episodes()))
+
+
 # ---------------------------------------------------- size-independent checks
 def test_full_size_index_stream_properties():
     """BASELINE S3-sized draw (1e6-row ring, 6 x 4096 indices): bit-exact vs
