@@ -195,8 +195,10 @@ int mdp_set_graphs(mdp_handle* h, int32_t on);
 int mdp_train_step(mdp_handle* h, int32_t rounds);
 /* n consecutive training steps (rounds[i] update rounds after step i's
  * rollout, exactly as n mdp_train_step calls) replayed as ONE graph, keyed
- * by the round counts: saves the graph-launch boundary between steps.  Steps
- * with 0 rounds, profiling or eager collectives run one by one.  launch = 0:
+ * by the round counts: saves the graph-launch boundary between steps.  A step
+ * with 0 rounds is its rollout launch alone inside the graph; before the first
+ * (eager) training step, with profiling or eager collectives the steps run
+ * one by one.  launch = 0:
  * only capture and instantiate the graph (nothing runs), so a timed region
  * replays graphs made ahead of it. */
 int mdp_train_steps(mdp_handle* h, int32_t n, const int32_t* rounds, int32_t launch);
