@@ -3,7 +3,7 @@
 # maddpg_amd/libmaddpg_hip_<name>.so (the A/B partner of tools/ab_lib.sh):
 #   bash tools/build_variant.sh wt -DMDP_NT_SLAB=2
 # Timing-only experiments (-DMDP_EXP_<NAME>: TPRE, R32, BF6, ONE_TACT,
-# NO_CRITQ, NOLOAD, NOMFMA, SLAB_NONE, SLAB_HALF, NOLOAD_R) are not in the product sources: their code
+# NO_CRITQ, NOLOAD, NOMFMA, SLAB_NONE, SLAB_HALF, NOLOAD_R, DW_NONE) are not in the product sources: their code
 # is tools/variants/mdp_exp.patch, applied to the scratch copy here whenever a
 # -DMDP_EXP_ flag is given (tools/variants/strip_exp.py made it).
 # Run here, not on the GPU box.
