@@ -53,10 +53,13 @@ def main():
     ap.add_argument("--scenario-adversaries", type=int, default=None)
     ap.add_argument("--num-adversaries", type=int, default=0)
     ap.add_argument("--adv-policy", default="maddpg")
+    ap.add_argument("--num-units", type=int, default=64)
+    ap.add_argument("--batch-size", type=int, default=1024)
     ap.add_argument("--update-mode", choices=["strict", "throughput"], default="strict")
     a = ap.parse_args()
     print(json.dumps(curve(a.scenario, a.num_envs, a.episodes, a.seed, a.num_agents, a.scenario_adversaries,
-                           a.num_adversaries, update_mode=a.update_mode, adv_policy=a.adv_policy)), flush=True)
+                           a.num_adversaries, batch_size=a.batch_size, num_units=a.num_units,
+                           update_mode=a.update_mode, adv_policy=a.adv_policy)), flush=True)
 
 
 if __name__ == "__main__":
