@@ -18,8 +18,6 @@ from ._lib import MdpConfig, MdpTensorInfo
 
 TENSOR_NAMES = ("W1", "b1", "W2", "b2", "W3", "b3")
 
-
-
 # the dtypes of update()'s return value in the reference (maddpg.py:196):
 # q_loss, p_loss are the fp32 scalars U.function fetches from TF1 (:91, :54-56);
 # np.mean(target_q_next) is the mean of an fp32 array (fp32, :185); the mean
@@ -30,6 +28,7 @@ UPDATE_STAT_DTYPES = (np.float32, np.float32, np.float64, np.float64, np.float32
 def update_stats(vals):
     """the 6 device stats (fp64, mdp_get_stats) as the reference's list of numpy scalars"""
     return [dt(v) for dt, v in zip(UPDATE_STAT_DTYPES, list(vals))]
+
 
 class Engine:
     def __init__(self, obs_dims, local_q=None, *, num_units=64, batch_size=1024, max_episode_len=25,
