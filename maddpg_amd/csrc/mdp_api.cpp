@@ -2157,11 +2157,14 @@ int mdp_env_reset(mdp_handle* h) {
 
 // pf_out: an extra rollout workgroup draws pf_count indices for the step's
 // first round against the post-step ring length (the draw leaves the critical path)
+// nsteps > 1: that many consecutive steps without update rounds in one launch
+// (rollout_multi_ok: one env workgroup, the policies' own actions, no draw)
 static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* u_dev, float* bench = nullptr,
-                           int32_t* pf_out = nullptr, int pf_count = 0) {
+                           int32_t* pf_out = nullptr, int pf_count = 0, int nsteps = 1) {
   RolloutArgs a;
   a.pf_out = pf_out;
   a.pf_count = pf_out ? pf_count : 0;
+  a.nsteps = nsteps;
   a.topo = h->L.topo;
   a.env = h->L.env;
   a.theta = h->theta;
@@ -2187,6 +2190,9 @@ static int env_step_launch(mdp_handle* h, const float* act_in_dev, const float* 
   HIPCHK(h, mdp_launch_rollout(a, h->L.topo.H, lds_rollout_bytes(h->L.topo), h->stream));
   return 0;
 }
+
+// several env steps per k_rollout launch need every env copy in one workgroup
+static bool rollout_multi_ok(const mdp_handle* h) { return h->cfg.num_envs <= 16; }  // k_rollout: 16 envs per workgroup (MDP_R)
 
 static void advance_ring_mirror(mdp_handle* h) {
   const int64_t cap = h->cfg.capacity, E = h->cfg.num_envs;
@@ -2296,7 +2302,19 @@ static int multi_graph(mdp_handle* h, const std::vector<int>& ks, hipGraphExec_t
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   h->capturing = true;
   int rc = 0;
-  for (size_t i = 0; i < ks.size() && !rc; ++i) rc = step_launches(h, ks[i]);
+  for (size_t i = 0; i < ks.size() && !rc;) {
+    // a stretch of steps without update rounds (one env copy: 99 of every 100)
+    // as one rollout launch of that many steps, when the envs fit one workgroup
+    size_t j = i;
+    while (j < ks.size() && ks[j] == 0 && (int)(j - i) < 64) ++j;
+    if (j - i > 1 && rollout_multi_ok(h)) {
+      rc = env_step_launch(h, nullptr, nullptr, nullptr, nullptr, 0, (int)(j - i));
+      i = j;
+    } else {
+      rc = step_launches(h, ks[i]);
+      ++i;
+    }
+  }
   h->capturing = false;
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(h->stream, &g);

@@ -222,6 +222,9 @@ struct RolloutArgs {
   // randint draws against the ring length after this step) beside the envs
   int pf_count;
   int32_t* pf_out;
+  // consecutive env steps in this launch (1; > 1 only with one env workgroup,
+  // no draw, no bench records and the policies' own actions)
+  int nsteps;
 };
 
 struct EnvResetArgs {

@@ -761,15 +761,18 @@ __global__ __launch_bounds__(256) void k_env_obs(EnvObsArgs a) {
 // the last workgroup to arrive advances the ring and the env step counter
 __device__ __forceinline__ void rollout_finish(const RolloutArgs& a, int64_t next, int64_t len) {
   if (last_block(a.ticket) && threadIdx.x == 0) {
-    a.ctl->next = (next + a.E) % a.cap;
-    a.ctl->len = len + a.E < a.cap ? len + a.E : a.cap;
-    a.ctl->env_steps += 1;
+    const int64_t moved = (int64_t)a.nsteps * a.E;  // a.nsteps env steps in this launch
+    a.ctl->next = (next + moved) % a.cap;
+    a.ctl->len = len + moved < a.cap ? len + moved : a.cap;
+    a.ctl->env_steps += (uint64_t)a.nsteps;
     a.ctl->episodes += atomicExch(&a.ctl->ep_pending, 0u);
     *a.ticket = 0u;
   }
 }
 
-template <int H>
+// MULTI: the a.nsteps > 1 instantiation (the one-step launch keeps its
+// straight-line schedule: a run-time loop around the body cost it 1.3 us)
+template <int H, bool MULTI>
 __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   MDP_TL_ROLLOUT();
@@ -855,8 +858,21 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
       sv[r * 2 * MDP_MAX_ENT + c] = vv[u];
     }
   }
-  for (int q = tid; q < MDP_R * ldr; q += MDP_NT) rowt[q] = 0.f;
   if (tid < MDP_R) sgoal[tid] = (int)ctr_use((uint32_t)goal);
+  // a.nsteps > 1 (one env workgroup, no draw, no injected actions: the host's
+  // mdp_rollout_steps_ok) runs that many consecutive env steps of a stretch
+  // without update rounds, the env state kept in LDS and registers between
+  // them; each step is exactly the launch's one step (same counters, same order)
+  __shared__ int s_nterm;  // this step's finished episodes (lockstep log slots)
+  int ep_done = 0;         // episodes finished in this launch's earlier steps
+  const int nsteps = MULTI ? a.nsteps : 1;
+  for (int sidx = 0; sidx < nsteps; ++sidx) {
+  if (MULTI && sidx > 0) __syncthreads();  // the previous step's replay rows are out of rowt
+  // this step's counter, read where it is used (an opaque VGPR, as the Ctl fields above)
+  auto step_s = [&]() { return ctr_use(step_raw) + (uint32_t)sidx; };
+  const int64_t next_s = next_raw + (int64_t)sidx * a.E;
+  for (int q = tid; q < MDP_R * ldr; q += MDP_NT) rowt[q] = 0.f;
+  if (MULTI && tid == 0) s_nterm = 0;
   __syncthreads();
   // observations, one thread per (env, agent)
   static_assert(MDP_R * MDP_MAX_AGENTS <= MDP_NT, "rollout obs: one pass");
@@ -898,7 +914,7 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
             for (int k = 0; k < MDP_ACT_DIM; ++k)
               u[k] = lane < nvalid ? a.u_in[((int64_t)(e0 + lane) * n + j) * MDP_ACT_DIM + k] : 0.5f;
           } else {
-            uniforms5(a.seed, 0x10000u | (uint32_t)j, ctr_use(step_raw), (uint32_t)(a.env_base + e0 + lane), u);
+            uniforms5(a.seed, 0x10000u | (uint32_t)j, step_s(), (uint32_t)(a.env_base + e0 + lane), u);
           }
         }
         float* h1j = hpar + j * (2 * MDP_R * MDP_RLH + MDP_R * 8);
@@ -957,7 +973,7 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
           for (int k = 0; k < MDP_ACT_DIM; ++k)
             u[k] = tid < nvalid ? a.u_in[((int64_t)(e0 + tid) * n + j) * MDP_ACT_DIM + k] : 0.5f;
         } else {
-          uniforms5(a.seed, 0x10000u | (uint32_t)j, ctr_use(step_raw), (uint32_t)(a.env_base + e0 + tid), u);
+          uniforms5(a.seed, 0x10000u | (uint32_t)j, step_s(), (uint32_t)(a.env_base + e0 + tid), u);
         }
         gumbel_softmax5(lg + tid * 8, u, dst);
       }
@@ -992,15 +1008,21 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
     term = st >= E.max_ep_len;
     if (term) {  // terminal -> log episode, env.reset() (train.py:127-133)
       const uint32_t q = atomicAdd(&a.ctl->ep_pending, 1u);
-      const int64_t slot = ep_base_raw + (a.eplog_by_env ? (int64_t)e : (int64_t)q);
+      const int64_t slot = ep_base_raw + (a.eplog_by_env ? (int64_t)(ep_done + e) : (int64_t)q);
       float* lgp = a.eplog + (slot % a.eplog_cap) * (1 + n);
       lgp[0] = tot;
       for (int j = 0; j < n; ++j) {
         lgp[1 + j] = epr[tid * MDP_MAX_AGENTS + j];
         a.ep_rew[(int64_t)e * n + j] = 0.f;
+        if (MULTI) epr[tid * MDP_MAX_AGENTS + j] = 0.f;
+      }
+      if (MULTI) {
+        atomicAdd(&s_nterm, 1);
+        ep_st = 0;
       }
     } else {
       a.ep_step[e] = st;
+      if (MULTI) ep_st = st;
     }
   } else if (tid >= 64 && tid - 64 < nvalid * n) {
     const int q = tid - 64, r = q / n, j = q - r * n;
@@ -1008,13 +1030,18 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   }
   static_assert(64 + MDP_R * MDP_MAX_AGENTS <= MDP_NT, "rollout obs': one pass on waves 1..");
   __syncthreads();
+  if (MULTI) ep_done += s_nterm;
   if (term) {
     const int e = e0 + tid;
     int32_t g;
-    env_reset_one(E, a.seed, 0x20000u, ctr_use(step_raw), (uint32_t)(a.env_base + e), sp + tid * 2 * MDP_MAX_ENT,
+    env_reset_one(E, a.seed, 0x20000u, step_s(), (uint32_t)(a.env_base + e), sp + tid * 2 * MDP_MAX_ENT,
                   sv + tid * 2 * MDP_MAX_ENT, &g);
     a.goal[e] = g;
     a.ep_step[e] = 0;
+    if (MULTI) {
+      goal = g;
+      sgoal[tid] = g;
+    }
   }
   __syncthreads();
   MDP_STAMP(46);
@@ -1023,9 +1050,10 @@ __global__ __launch_bounds__(MDP_NT) void k_rollout(RolloutArgs a) {
   for (int q = tid; q < nvalid * v4; q += MDP_NT) {
     const int r = q / v4, c4 = q - r * v4;
     const float* s = rowt + r * ldr + c4 * 4;
-    const int64_t dst = (next_raw + e0 + r) % a.cap;
+    const int64_t dst = (next_s + e0 + r) % a.cap;
     *reinterpret_cast<float4*>(a.replay + dst * T.row_stride + c4 * 4) = make_float4(s[0], s[1], s[2], s[3]);
   }
+  }  // steps of the launch
   for (int q = tid; q < nvalid * 2 * ne; q += MDP_NT) {
     const int r = q / (2 * ne), c = q - r * 2 * ne;
     a.pos[(int64_t)(e0 + r) * 2 * ne + c] = sp[r * 2 * MDP_MAX_ENT + c];
@@ -1081,7 +1109,10 @@ __global__ __launch_bounds__(MDP_NT) void k_mlp_eval(EvalArgs a) {
 template <int H>
 static hipError_t launch_rollout_t(const RolloutArgs& a, int lds_bytes, hipStream_t s) {
   const int grid = (a.E + MDP_R - 1) / MDP_R + (a.pf_count > 0 ? 1 : 0);
-  mdp_launch(k_rollout<H>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
+  if (a.nsteps > 1)
+    mdp_launch(k_rollout<H, true>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
+  else
+    mdp_launch(k_rollout<H, false>, dim3(grid), dim3(MDP_NT), lds_bytes, s, a);
   MDP_CHECK_LAUNCH();
   return hipSuccess;
 }
@@ -1096,7 +1127,8 @@ static hipError_t launch_eval_t(const EvalArgs& a, int lds_bytes, hipStream_t s)
 static int set_lds_limit_done = 0;
 template <int H>
 static void raise_lds_limits() {
-  (void)hipFuncSetAttribute((const void*)k_rollout<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_rollout<H, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_rollout<H, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
   (void)hipFuncSetAttribute((const void*)k_mlp_eval<H>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
 }
 static void ensure_lds_limits() {

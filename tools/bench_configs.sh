@@ -9,7 +9,8 @@ TAG=${1:-cfg}
 O=gpurun_out/$TAG/configs
 mkdir -p $O
 B="python3 bench.py --no-cpu-baseline --no-gather-stage --no-configs2 --steps 20 --warmup 3"
-timeout -k 10 240 $B --steps 500 --scenario simple --num-agents 1 --num-envs 1 > $O/s1_simple_e1.json 2> $O/s1.err
+# configs[0]: one env copy, an episode (25 steps, 24 of them without a round) per graph replay, as train.py runs it
+timeout -k 10 240 $B --steps 1000 --step-group 25 --scenario simple --num-agents 1 --num-envs 1 > $O/s1_simple_e1.json 2> $O/s1.err
 timeout -k 10 240 $B > $O/s2_spread_e1024.json 2> $O/s2.err
 timeout -k 10 240 $B --num-envs 4096 > $O/s3_spread_e4096.json 2> $O/s3.err
 timeout -k 10 240 $B --scenario simple_adversary --num-envs 4096 --num-adversaries 1 --adv-policy ddpg \
