@@ -196,7 +196,8 @@ int mdp_train_step(mdp_handle* h, int32_t rounds);
 /* n consecutive training steps (rounds[i] update rounds after step i's
  * rollout, exactly as n mdp_train_step calls) replayed as ONE graph, keyed
  * by the round counts: saves the graph-launch boundary between steps.  A step
- * with 0 rounds is its rollout launch alone inside the graph; before the first
+ * with 0 rounds is its rollout launch alone inside the graph (a stretch of
+ * them one k_rollout launch of that many steps when num_envs <= 16); before the first
  * (eager) training step, with profiling or eager collectives the steps run
  * one by one.  launch = 0:
  * only capture and instantiate the graph (nothing runs), so a timed region
