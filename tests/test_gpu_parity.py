@@ -1016,16 +1016,22 @@ def test_train_steps_group_graph_equals_step_graphs(monkeypatch, general):
     assert a.episodes() == b.episodes()
 
 
-@pytest.mark.parametrize("E,every,gate_open", [(64, 100, True), (1, 100, True), (64, 100, False)])
-def test_train_steps_group_with_rollout_only_steps(E, every, gate_open):
+@pytest.mark.parametrize("scenario,E,every,gate_open,n,group", [
+    ("simple_spread", 64, 100, True, 12, 6), ("simple_spread", 1, 100, True, 120, 60),
+    ("simple_spread", 64, 100, False, 12, 6), ("simple_adversary", 16, 400, True, 60, 30),
+    ("simple_tag", 8, 200, True, 60, 30)])
+def test_train_steps_group_with_rollout_only_steps(scenario, E, every, gate_open, n, group):
     """Groups whose steps do not all train (64 transitions per step and a round
     per 100: rounds 1, 0, 1, 1, 0, ...; E = 1, the reference's own structure:
     one round in 100 steps; a group that starts below the replay gate): the
-    group graph == the steps one by one, bit for bit, and the episode log."""
+    group graph == the steps one by one, bit for bit, and the episode log.
+    With E <= 16 a stretch of steps without a round is ONE k_rollout launch of
+    that many steps (env state, returns and goals carried in LDS: the adversary's
+    goal landmark and tag's collisions across episode ends included)."""
     from maddpg_amd.runner import VecRunner
 
     def make():
-        r = VecRunner("simple_spread", E, batch_size=64, capacity=2000, seed=11, train_every=every)
+        r = VecRunner(scenario, E, batch_size=64, capacity=2000, seed=11, train_every=every)
         if gate_open:
             r.prefill()
             while r.step() == 0:              # the one eager training step
@@ -1033,13 +1039,12 @@ def test_train_steps_group_with_rollout_only_steps(E, every, gate_open):
         return r
 
     a, b = make(), make()
-    n = 120 if E == 1 else 12                 # E = 1: the next round is 100 steps after the eager one
-    pa_ = a.plan(n)
+    pa_ = a.plan(n)                           # E = 1: the next round is 100 steps after the eager one
     assert 0 in pa_ and (not gate_open or any(pa_)), pa_
     if gate_open:
-        sizes = a.prepare_steps(n, 60 if E == 1 else 6)
+        sizes = a.prepare_steps(n, group)
     else:                                     # below the gate: no eager step yet, groups fall back to one by one
-        sizes = [6] * (n // 6)
+        sizes = [group] * (n // group)
     ra = sum(a.steps(g) for g in sizes)
     rb = sum(b.step() for _ in range(n))
     assert ra == rb and a.train_step == b.train_step and a.rounds == b.rounds
